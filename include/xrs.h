@@ -1,0 +1,111 @@
+/*
+ * xrs.h — C-ABI of libxrs, the MI355X (gfx950) engine for xcube-resampling's
+ * per-chunk inner loops.
+ *
+ * Every compute entry point replaces one per-chunk seam of the reference
+ * (xcube-dev/xcube-resampling @ 2025-09-05, paths relative to its repo root):
+ * the dask block callables / numba kernels that do the pixel work.  Host code
+ * (the Python package `xcube_resampling_amd`, or any FFI: ctypes, cgo, JNI)
+ * keeps the reference's orchestration semantics and calls these functions on
+ * device buffers.
+ *
+ * Conventions
+ *  - All data pointers are DEVICE pointers (hipMalloc / torch CUDA tensors),
+ *    unless a parameter is documented as host memory.
+ *  - Shapes, strides and indices are int64_t; strides are in ELEMENTS.
+ *  - `stream` is a hipStream_t passed as void* (NULL = default stream).  Every
+ *    call is asynchronous and stream-ordered; no hidden allocation, no host
+ *    synchronisation inside (safe to capture in a hipGraph).
+ *  - Return value: XRS_OK (0) or a negative XRS_ERR_* code; the message is in
+ *    xrs_last_error() (thread-local).
+ *  - Data-dependent errors the reference raises from inside a block (e.g. the
+ *    IndexError of numpy fancy indexing in reproject.py:284) are reported by
+ *    OR-ing a bit into the caller-provided device word `err_flags`; the host
+ *    reads it after the stream is synchronised and raises the same exception.
+ */
+#ifndef XRS_H_
+#define XRS_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ---------------------------------------------------- */
+#define XRS_OK 0
+#define XRS_ERR_ARG (-1)      /* invalid argument (shape/dtype/method)       */
+#define XRS_ERR_HIP (-2)      /* HIP runtime error (launch failed, ...)      */
+#define XRS_ERR_NOTIMPL (-3)  /* method not implemented (reference: NotImplementedError) */
+
+/* ---- dtype codes ------------------------------------------------------- */
+#define XRS_DTYPE_U8 1
+#define XRS_DTYPE_I8 2
+#define XRS_DTYPE_U16 3
+#define XRS_DTYPE_I16 4
+#define XRS_DTYPE_U32 5
+#define XRS_DTYPE_I32 6
+#define XRS_DTYPE_I64 7
+#define XRS_DTYPE_F32 10
+#define XRS_DTYPE_F64 11
+
+/* ---- interpolation codes (constants.py:66-70) --------------------------- */
+#define XRS_INTERP_NEAREST 0
+#define XRS_INTERP_BILINEAR 1
+#define XRS_INTERP_TRIANGULAR 2
+
+/* ---- err_flags bits ------------------------------------------------------ */
+#define XRS_EFLAG_INDEX 1     /* numpy IndexError (window index out of range) */
+#define XRS_EFLAG_BAND 2      /* read outside the source band held on device  */
+
+/* library identification */
+const char* xrs_version(void);
+/* thread-local message of the last failing call ("" if none) */
+const char* xrs_last_error(void);
+
+/* -------------------------------------------------------------------------
+ * xrs_reproject — replaces `_reproject_block` (reproject.py:268-335) for ALL
+ * target tiles of one variable in one launch, and the per-tile source-window
+ * materialisation it depends on (`_reorganize_data_array_slice`,
+ * reproject.py:499-530: da.pad + copy) by bounds-checked reads that return
+ * `fill` outside the source (equivalent to the constant padding).
+ *
+ * Per target pixel (global row r, col c; tile t = (r/tile_h, c/tile_w)):
+ *   sx, sy = coordinate of the pixel centre in the source CRS
+ *            coord_mode 0 (separable): sx = src_x[c], sy = src_y[r]
+ *            coord_mode 1 (2-D):       sx = src_x[r*dst_w+c], sy = src_y[...]
+ *   ix = (sx - (double)tile_x0[t]) / x_res           (reproject.py:278)
+ *   iy = (sy - (double)tile_y0[t]) / -y_res          (reproject.py:279)
+ *   window index -> int16 as numpy, python-style negative wrap in
+ *   [-win, win), else IndexError (err_flags |= XRS_EFLAG_INDEX);
+ *   source row/col = tile_win[2t+1] + wy, tile_win[2t] + wx (unpadded);
+ *   outside [0,src_h) x [0,src_w) -> fill (the da.pad constant).
+ *   nearest: rint (half-even); bilinear: f64 lerps, source differences in the
+ *   source dtype; triangular: two-triangle plane, stored in the source dtype.
+ *
+ * src: (n, src_rows, src_w) with element strides (src_sn, src_sy, 1); row 0
+ *      of the buffer is global source row `src_row0` (a device may hold a band).
+ * dst: (n, row_end-row_begin, dst_w) with strides (dst_sn, dst_sy, 1); only
+ *      target rows [row_begin, row_end) are computed (multi-GPU row bands).
+ * tile_x0/tile_y0 (float32, ntiles), tile_win (int64, 2*ntiles: i0, j0 of
+ *      each tile's window in unpadded source indices): device memory,
+ *      ntiles = ceil(dst_h/tile_h) * ceil(dst_w/tile_w), row-major.
+ * dst_dtype: = src_dtype for nearest/triangular; float32 or float64 for
+ *      bilinear (the reference yields float64 there; float32 = declared dtype).
+ * ------------------------------------------------------------------------- */
+int xrs_reproject(const void* src, int src_dtype, int64_t n, int64_t src_h,
+                  int64_t src_w, int64_t src_row0, int64_t src_rows,
+                  int64_t src_sn, int64_t src_sy, void* dst, int dst_dtype,
+                  int64_t dst_h, int64_t dst_w, int64_t row_begin,
+                  int64_t row_end, int64_t dst_sn, int64_t dst_sy,
+                  int64_t tile_h, int64_t tile_w, const double* src_x,
+                  const double* src_y, int coord_mode, const float* tile_x0,
+                  const float* tile_y0, const int64_t* tile_win,
+                  int64_t win_h, int64_t win_w, double x_res, double y_res,
+                  int interp, double fill, int32_t* err_flags, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* XRS_H_ */

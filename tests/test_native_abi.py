@@ -1,0 +1,54 @@
+"""CPU checks of the C-ABI library: it loads and exports every symbol that
+include/xrs.h declares (no compute calls: there is no GPU here)."""
+
+import ast
+import os
+
+import pytest
+
+from conftest import ROOT
+
+
+def test_library_exports_every_declared_symbol():
+    from xcube_resampling_amd import _native
+
+    names = _native.declared_symbols()
+    assert "xrs_reproject" in names and "xrs_last_error" in names
+    lib = _native.load_library()
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, f"declared in include/xrs.h but not exported: {missing}"
+    assert lib.xrs_version().decode().startswith("xrs ")
+    # every declared symbol has a ctypes signature in the binding
+    assert set(names) <= set(_native._SIGNATURES), set(names) - set(_native._SIGNATURES)
+
+
+def test_product_package_never_imports_the_oracle():
+    pkg = os.path.join(ROOT, "xcube-resampling_amd")
+    offenders = []
+    for dirpath, _, files in os.walk(pkg):
+        for f in files:
+            if not f.endswith(".py"):
+                continue
+            path = os.path.join(dirpath, f)
+            tree = ast.parse(open(path).read())
+            for node in ast.walk(tree):
+                mods = []
+                if isinstance(node, ast.Import):
+                    mods = [a.name for a in node.names]
+                elif isinstance(node, ast.ImportFrom) and node.module:
+                    mods = [node.module]
+                if any(m == "oracle" or m.startswith("oracle.") for m in mods):
+                    offenders.append(path)
+    assert not offenders, offenders
+
+
+def test_compute_without_gpu_fails_loudly():
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    from xcube_resampling_amd.device import require_device
+    from xcube_resampling_amd._native import NativeLibraryError
+
+    with pytest.raises(NativeLibraryError, match="no HIP device"):
+        require_device()

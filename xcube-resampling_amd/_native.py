@@ -1,0 +1,128 @@
+"""ctypes binding of libxrs.so (the HIP kernels behind include/xrs.h).
+
+The library is the product: there is no CPU fallback.  If it is missing, or
+no HIP device is present, every compute call raises ``NativeLibraryError``.
+
+Load order matters: ``torch`` is imported first so that the process holds ONE
+HIP runtime.  libxrs.so's DT_NEEDED ``libamdhip64.so.7`` then resolves to the
+runtime torch already loaded (same SONAME), so device pointers and streams
+created by torch are valid in the kernels' runtime.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+import threading
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("XRS_LIBRARY", os.path.join(_HERE, "lib", "libxrs.so"))
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "xrs.h")
+
+XRS_OK = 0
+XRS_ERR_ARG = -1
+XRS_ERR_HIP = -2
+XRS_ERR_NOTIMPL = -3
+
+XRS_EFLAG_INDEX = 1
+XRS_EFLAG_BAND = 2
+
+INTERP_CODES = {"nearest": 0, "bilinear": 1, "triangular": 2}
+
+DTYPE_CODES = {
+    np.dtype(np.uint8): 1,
+    np.dtype(np.int8): 2,
+    np.dtype(np.uint16): 3,
+    np.dtype(np.int16): 4,
+    np.dtype(np.uint32): 5,
+    np.dtype(np.int32): 6,
+    np.dtype(np.int64): 7,
+    np.dtype(np.float32): 10,
+    np.dtype(np.float64): 11,
+}
+
+
+class NativeLibraryError(RuntimeError):
+    """libxrs.so could not be loaded or a HIP call failed."""
+
+
+_c_i64 = ctypes.c_int64
+_c_int = ctypes.c_int
+_c_dbl = ctypes.c_double
+_c_ptr = ctypes.c_void_p
+
+# argument lists, in declaration order of include/xrs.h
+_SIGNATURES = {
+    "xrs_version": (ctypes.c_char_p, []),
+    "xrs_last_error": (ctypes.c_char_p, []),
+    "xrs_reproject": (_c_int, [
+        _c_ptr, _c_int, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64,  # src
+        _c_ptr, _c_int, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64,          # dst
+        _c_i64, _c_i64,                                                          # tile
+        _c_ptr, _c_ptr, _c_int,                                                  # coords
+        _c_ptr, _c_ptr, _c_ptr, _c_i64, _c_i64,                                  # tile tables
+        _c_dbl, _c_dbl, _c_int, _c_dbl, _c_ptr, _c_ptr,                          # res, interp...
+    ]),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+def declared_symbols(header: str = HEADER_PATH) -> list[str]:
+    """Names of all functions declared in include/xrs.h."""
+    with open(header) as f:
+        text = f.read()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\**\s+\**(xrs_\w+)\s*\(", text, re.M)))
+
+
+def load_library(path: str = LIB_PATH):
+    """Load libxrs.so without requiring a GPU (symbol checks, CPU tests)."""
+    if not os.path.exists(path):
+        raise NativeLibraryError(
+            f"libxrs.so not found at {path}: build it with "
+            f"`make -C xcube-resampling_amd/csrc` (or __graft_entry__.build())"
+        )
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in _SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+def lib():
+    """The loaded library, bound to torch's HIP runtime."""
+    global _lib
+    if _lib is None:
+        with _lock:
+            if _lib is None:
+                import torch  # noqa: F401  (must precede the CDLL: one HIP runtime)
+                _lib = load_library()
+    return _lib
+
+
+def last_error() -> str:
+    msg = lib().xrs_last_error()
+    return msg.decode() if msg else ""
+
+
+def check(rc: int, what: str) -> None:
+    if rc == XRS_OK:
+        return
+    msg = last_error()
+    if rc == XRS_ERR_NOTIMPL:
+        raise NotImplementedError(msg)
+    if rc == XRS_ERR_ARG:
+        raise ValueError(f"{what}: {msg}")
+    raise NativeLibraryError(f"{what}: {msg}")
+
+
+def dtype_code(dtype) -> int:
+    try:
+        return DTYPE_CODES[np.dtype(dtype)]
+    except KeyError:
+        raise TypeError(f"unsupported dtype {dtype!r}") from None

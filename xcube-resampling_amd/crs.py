@@ -1,0 +1,329 @@
+"""Coordinate reference systems and transformations for the resampling engine.
+
+The reference reaches PROJ through ``pyproj`` (``pyproj.CRS``,
+``pyproj.Transformer.from_crs(..., always_xy=True)``; call sites
+reproject.py:124-126,347,398,483 and rectify.py:196-203).  Neither pyproj nor
+PROJ's database is available here or on the GPU box, so this module restates
+the small part of PROJ the engine needs:
+
+* a registry of the CRSs the engine supports (geographic WGS 84 in both axis
+  orders, and Web Mercator), with the attributes the reference reads
+  (``is_geographic``, ``name``, ``equals``, ``to_cf``, ``axis_info``);
+* ``Transformer`` with ``transform`` and ``transform_bounds`` following PROJ's
+  formulas: spherical Mercator (``webmerc``: merc_s_forward / merc_s_inverse
+  with ``a = 6378137``; coordinates de-scaled by the reciprocal ``ra = 1/a``;
+  radians <-> degrees through a precomputed ``unitconvert`` factor) and PROJ's
+  ``proj_trans_bounds`` edge densification (21 points per edge by default).
+
+If ``pyproj`` is importable, ``CRS.from_pyproj`` accepts pyproj objects for the
+supported codes.  Transformations between unsupported CRS pairs raise
+``NotImplementedError`` instead of silently approximating.
+"""
+
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import numpy as np
+
+# PROJ constants (proj_internal.h / unitconvert.cpp)
+_DEG_TO_RAD = 0.017453292519943296
+_RAD_TO_DEG_FACTOR = 1.0 / _DEG_TO_RAD   # unitconvert xy_factor rad -> deg
+_WGS84_A = 6378137.0
+_WGS84_RF = 298.257223563
+
+
+@dataclass(frozen=True)
+class AxisInfo:
+    name: str
+    abbrev: str
+    direction: str
+    unit_name: str
+
+
+@dataclass(frozen=True, eq=False)
+class CRS:
+    """A coordinate reference system known to the engine.
+
+    Mirrors the subset of ``pyproj.CRS`` the reference uses
+    (gridmapping/base.py:398-404, utils.py:187-189, cfconv.py).
+    """
+
+    authority: str          # "EPSG" or "OGC"
+    code: str               # "4326", "CRS84", "3857"
+    name: str
+    kind: str               # "geographic" | "webmerc"
+    axis_order: str         # "latlon" | "lonlat" | "en"
+    cf: dict = field(default_factory=dict)
+
+    # ---- pyproj-like API ------------------------------------------------
+    @property
+    def is_geographic(self) -> bool:
+        return self.kind == "geographic"
+
+    @property
+    def is_projected(self) -> bool:
+        return not self.is_geographic
+
+    @property
+    def srs(self) -> str:
+        return f"{self.authority}:{self.code}"
+
+    def to_string(self) -> str:
+        return self.srs
+
+    def to_epsg(self) -> int | None:
+        return int(self.code) if self.authority == "EPSG" else None
+
+    @property
+    def axis_info(self) -> list[AxisInfo]:
+        if self.is_geographic:
+            lat = AxisInfo("Geodetic latitude", "Lat", "north", "degree")
+            lon = AxisInfo("Geodetic longitude", "Lon", "east", "degree")
+            return [lat, lon] if self.axis_order == "latlon" else [lon, lat]
+        return [
+            AxisInfo("Easting", "X", "east", "metre"),
+            AxisInfo("Northing", "Y", "north", "metre"),
+        ]
+
+    def to_cf(self) -> dict:
+        return dict(self.cf)
+
+    def equals(self, other, ignore_axis_order: bool = False) -> bool:
+        other = _as_crs(other)
+        if other is None:
+            return False
+        same_datum_kind = self.kind == other.kind
+        if not same_datum_kind:
+            return False
+        if ignore_axis_order:
+            return True
+        return self.axis_order == other.axis_order
+
+    def __eq__(self, other) -> bool:
+        try:
+            other = _as_crs(other)
+        except (ValueError, TypeError):
+            return False
+        return other is not None and self.equals(other)
+
+    def __hash__(self) -> int:
+        return hash((self.kind, self.axis_order))
+
+    def __repr__(self) -> str:
+        return f"<CRS {self.srs}: {self.name}>"
+
+    __str__ = to_string
+
+    # ---- construction ------------------------------------------------------
+    @classmethod
+    def from_string(cls, value: str) -> "CRS":
+        key = value.strip().upper().replace(" ", "")
+        if key in _ALIASES:
+            return _REGISTRY[_ALIASES[key]]
+        raise ValueError(f"unsupported CRS: {value!r}")
+
+    @classmethod
+    def from_epsg(cls, code: int | str) -> "CRS":
+        return cls.from_string(f"EPSG:{int(code)}")
+
+    @classmethod
+    def from_user_input(cls, value) -> "CRS":
+        crs = _as_crs(value)
+        if crs is None:
+            raise ValueError(f"unsupported CRS: {value!r}")
+        return crs
+
+    @classmethod
+    def from_cf(cls, attrs: dict) -> "CRS":
+        """Recognise a CRS from CF grid-mapping attributes (cfconv.py:66-212)."""
+        for key in ("crs_wkt", "spatial_ref"):
+            wkt = attrs.get(key)
+            if isinstance(wkt, str):
+                for crs in _REGISTRY.values():
+                    if crs.cf.get("crs_wkt") == wkt:
+                        return crs
+                if "Pseudo-Mercator" in wkt or "Popular Visualisation" in wkt:
+                    return _REGISTRY["EPSG:3857"]
+                if wkt.startswith("GEOGCRS") or wkt.startswith("GEOGCS"):
+                    if "CRS84" in wkt:
+                        return _REGISTRY["OGC:CRS84"]
+                    return _REGISTRY["EPSG:4326"]
+        gm_name = attrs.get("grid_mapping_name")
+        if gm_name == "latitude_longitude":
+            return _REGISTRY["EPSG:4326"]
+        if gm_name == "mercator" and float(attrs.get("semi_major_axis", _WGS84_A)) == _WGS84_A \
+                and float(attrs.get("inverse_flattening", 0.0)) == 0.0:
+            return _REGISTRY["EPSG:3857"]
+        raise ValueError(f"unsupported CF grid mapping: {attrs!r}")
+
+
+def _geographic_cf(name: str, crs_wkt: str) -> dict:
+    return dict(
+        crs_wkt=crs_wkt,
+        semi_major_axis=_WGS84_A,
+        semi_minor_axis=6356752.314245179,
+        inverse_flattening=_WGS84_RF,
+        reference_ellipsoid_name="WGS 84",
+        longitude_of_prime_meridian=0.0,
+        prime_meridian_name="Greenwich",
+        geographic_crs_name=name,
+        horizontal_datum_name="World Geodetic System 1984 ensemble",
+        grid_mapping_name="latitude_longitude",
+    )
+
+
+_WKT_4326 = 'GEOGCRS["WGS 84",ENSEMBLE["World Geodetic System 1984 ensemble"],ID["EPSG",4326]]'
+_WKT_CRS84 = 'GEOGCRS["WGS 84 (CRS84)",ENSEMBLE["World Geodetic System 1984 ensemble"],ID["OGC","CRS84"]]'
+_WKT_3857 = 'PROJCRS["WGS 84 / Pseudo-Mercator",BASEGEOGCRS["WGS 84"],CONVERSION["Popular Visualisation Pseudo-Mercator"],ID["EPSG",3857]]'
+
+_REGISTRY: dict[str, CRS] = {
+    "EPSG:4326": CRS("EPSG", "4326", "WGS 84", "geographic", "latlon",
+                     _geographic_cf("WGS 84", _WKT_4326)),
+    "OGC:CRS84": CRS("OGC", "CRS84", "WGS 84 (CRS84)", "geographic", "lonlat",
+                     _geographic_cf("WGS 84 (CRS84)", _WKT_CRS84)),
+    "EPSG:3857": CRS("EPSG", "3857", "WGS 84 / Pseudo-Mercator", "webmerc", "en",
+                     dict(crs_wkt=_WKT_3857, semi_major_axis=_WGS84_A,
+                          semi_minor_axis=6356752.314245179,
+                          inverse_flattening=_WGS84_RF,
+                          reference_ellipsoid_name="WGS 84",
+                          longitude_of_prime_meridian=0.0,
+                          prime_meridian_name="Greenwich",
+                          geographic_crs_name="WGS 84",
+                          horizontal_datum_name="World Geodetic System 1984 ensemble",
+                          projected_crs_name="WGS 84 / Pseudo-Mercator",
+                          grid_mapping_name="mercator",
+                          standard_parallel=0.0,
+                          longitude_of_projection_origin=0.0,
+                          false_easting=0.0, false_northing=0.0)),
+}
+_ALIASES = {
+    "EPSG:4326": "EPSG:4326", "WGS84": "EPSG:4326", "4326": "EPSG:4326",
+    "OGC:CRS84": "OGC:CRS84", "CRS84": "OGC:CRS84", "OGC:1.3:CRS84": "OGC:CRS84",
+    "URN:OGC:DEF:CRS:OGC:1.3:CRS84": "OGC:CRS84",
+    "EPSG:3857": "EPSG:3857", "3857": "EPSG:3857", "EPSG:900913": "EPSG:3857",
+}
+
+CRS_WGS84 = _REGISTRY["EPSG:4326"]
+CRS_CRS84 = _REGISTRY["OGC:CRS84"]
+CRS_WEBMERC = _REGISTRY["EPSG:3857"]
+
+
+def _as_crs(value) -> CRS | None:
+    if value is None:
+        return None
+    if isinstance(value, CRS):
+        return value
+    if isinstance(value, str):
+        return CRS.from_string(value)
+    if isinstance(value, int):
+        return CRS.from_epsg(value)
+    # pyproj.CRS, if pyproj is installed: map by authority code
+    to_authority = getattr(value, "to_authority", None)
+    if callable(to_authority):
+        auth = to_authority()
+        if auth:
+            return CRS.from_string(f"{auth[0]}:{auth[1]}")
+    raise ValueError(f"unsupported CRS: {value!r}")
+
+
+def normalize_crs(crs) -> CRS:
+    """gridmapping/helpers.py:59-63 (`_normalize_crs`)."""
+    return CRS.from_user_input(crs)
+
+
+# --------------------------------------------------------------------------
+# Transformations (always_xy=True semantics: x = lon/easting, y = lat/northing)
+# --------------------------------------------------------------------------
+
+def webmerc_inverse(x, y):
+    """EPSG:3857 -> geographic degrees (PROJ merc_s_inverse, webmerc).
+
+    PROJ de-scales by the reciprocal of the semi-major axis (inv_prepare:
+    ``x * ra``) then ``lam = x``, ``phi = atan(sinh(y))`` (k0 = 1), then
+    unitconvert multiplies radians by the precomputed rad->deg factor.
+    """
+    ra = 1.0 / _WGS84_A
+    x = np.asarray(x, dtype=np.float64)
+    y = np.asarray(y, dtype=np.float64)
+    lam = x * ra
+    phi = np.arctan(np.sinh(y * ra))
+    return lam * _RAD_TO_DEG_FACTOR, phi * _RAD_TO_DEG_FACTOR
+
+
+def webmerc_forward(lon, lat):
+    """Geographic degrees -> EPSG:3857 (PROJ merc_s_forward, webmerc)."""
+    lam = np.asarray(lon, dtype=np.float64) * _DEG_TO_RAD
+    phi = np.asarray(lat, dtype=np.float64) * _DEG_TO_RAD
+    x = lam
+    y = np.arcsinh(np.tan(phi))
+    return _WGS84_A * x, _WGS84_A * y
+
+
+class Transformer:
+    """Subset of ``pyproj.Transformer`` used by the reference."""
+
+    def __init__(self, crs_from: CRS, crs_to: CRS):
+        self.source_crs = crs_from
+        self.target_crs = crs_to
+        a, b = crs_from.kind, crs_to.kind
+        if a == b:
+            self._fn = None
+        elif a == "webmerc" and b == "geographic":
+            self._fn = webmerc_inverse
+        elif a == "geographic" and b == "webmerc":
+            self._fn = webmerc_forward
+        else:
+            raise NotImplementedError(
+                f"transformation {crs_from.srs} -> {crs_to.srs} is not supported"
+            )
+
+    @classmethod
+    def from_crs(cls, crs_from, crs_to, always_xy: bool = False) -> "Transformer":
+        if not always_xy:
+            raise NotImplementedError("only always_xy=True is supported")
+        return cls(normalize_crs(crs_from), normalize_crs(crs_to))
+
+    @property
+    def is_identity(self) -> bool:
+        return self._fn is None
+
+    @property
+    def is_separable(self) -> bool:
+        """x' depends only on x and y' only on y (true for every supported pair)."""
+        return True
+
+    def transform(self, xx, yy):
+        xx = np.asarray(xx, dtype=np.float64)
+        yy = np.asarray(yy, dtype=np.float64)
+        if self._fn is None:
+            return xx.copy(), yy.copy()
+        return self._fn(xx, yy)
+
+    def transform_x(self, x):
+        """Separable x part: x' for a vector of x (y is irrelevant)."""
+        return self.transform(x, np.zeros_like(np.asarray(x, dtype=np.float64)))[0]
+
+    def transform_y(self, y):
+        """Separable y part: y' for a vector of y (x is irrelevant)."""
+        return self.transform(np.zeros_like(np.asarray(y, dtype=np.float64)), y)[1]
+
+    def transform_bounds(self, left, bottom, right, top, densify_pts: int = 21):
+        """PROJ proj_trans_bounds: densify the four edges, transform, min/max."""
+        side = densify_pts + 1
+        dx = (right - left) / side
+        dy = (top - bottom) / side
+        xs = np.empty(4 * side)
+        ys = np.empty(4 * side)
+        k = np.arange(side, dtype=np.float64)
+        xs[0:side], ys[0:side] = left, top - k * dy
+        xs[side:2 * side], ys[side:2 * side] = left + k * dx, bottom
+        xs[2 * side:3 * side], ys[2 * side:3 * side] = right, bottom + k * dy
+        xs[3 * side:], ys[3 * side:] = right - k * dx, top
+        tx, ty = self.transform(xs, ys)
+        ok = np.isfinite(tx) & np.isfinite(ty)
+        if not np.any(ok):
+            return (math.inf, math.inf, math.inf, math.inf)
+        tx, ty = tx[ok], ty[ok]
+        return (float(tx.min()), float(ty.min()), float(tx.max()), float(ty.max()))

@@ -1,0 +1,133 @@
+// xrs_common.hpp — shared device/host helpers for the libxrs HIP kernels (gfx950).
+//
+// Everything here restates numpy/x86 scalar semantics that the reference's CPU
+// path relies on, so the kernels reproduce the reference bit for bit:
+//   * float64 -> integer casts follow numpy-on-x86 (cvttsd2si to int32, then
+//     keep the low bits; NaN / out-of-range -> INT32_MIN before narrowing),
+//   * arithmetic differences of two source values are evaluated in the source
+//     dtype (numpy `a - b` on two uint8 arrays wraps, on float32 rounds to f32),
+//   * no FMA contraction: the library is compiled with -ffp-contract=off.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/xrs.h"
+
+namespace xrs {
+
+// ---- numpy float64 -> int casts (x86 semantics) -------------------------
+// numpy lowers float64 -> {int8,int16,uint8,uint16,int32} through a 32-bit
+// truncating conversion (cvttsd2si): NaN and values outside int32 produce the
+// "integer indefinite" 0x80000000, which is then narrowed to the target width.
+__device__ __host__ inline int32_t f64_to_i32_x86(double x) {
+  if (!(x >= -2147483648.0 && x < 2147483648.0)) return INT32_MIN;  // also NaN
+  return (int32_t)x;  // truncation toward zero
+}
+__device__ __host__ inline int64_t f64_to_i64_x86(double x) {
+  if (!(x >= -9223372036854775808.0 && x < 9223372036854775808.0)) return INT64_MIN;
+  return (int64_t)x;
+}
+// numpy float64 -> int16 (reproject.py:282-283,286-289,316-319 index casts)
+__device__ __host__ inline int16_t f64_to_i16_np(double x) {
+  return (int16_t)(uint16_t)(uint32_t)f64_to_i32_x86(x);
+}
+
+template <typename T> struct Conv;
+template <> struct Conv<float> {
+  __device__ static inline float from_f64(double v) { return (float)v; }
+  __device__ static inline double to_f64(float v) { return (double)v; }
+  __device__ static inline float diff(float a, float b) { return a - b; }
+};
+template <> struct Conv<double> {
+  __device__ static inline double from_f64(double v) { return v; }
+  __device__ static inline double to_f64(double v) { return v; }
+  __device__ static inline double diff(double a, double b) { return a - b; }
+};
+#define XRS_SMALL_INT_CONV(T)                                                  \
+  template <> struct Conv<T> {                                                 \
+    __device__ static inline T from_f64(double v) {                            \
+      return (T)(uint32_t)f64_to_i32_x86(v);                                   \
+    }                                                                          \
+    __device__ static inline double to_f64(T v) { return (double)v; }         \
+    __device__ static inline T diff(T a, T b) { return (T)(a - b); }           \
+  };
+XRS_SMALL_INT_CONV(uint8_t)
+XRS_SMALL_INT_CONV(int8_t)
+XRS_SMALL_INT_CONV(uint16_t)
+XRS_SMALL_INT_CONV(int16_t)
+XRS_SMALL_INT_CONV(int32_t)
+#undef XRS_SMALL_INT_CONV
+template <> struct Conv<uint32_t> {
+  __device__ static inline uint32_t from_f64(double v) {
+    return (uint32_t)(uint64_t)f64_to_i64_x86(v);
+  }
+  __device__ static inline double to_f64(uint32_t v) { return (double)v; }
+  __device__ static inline uint32_t diff(uint32_t a, uint32_t b) { return a - b; }
+};
+template <> struct Conv<int64_t> {
+  __device__ static inline int64_t from_f64(double v) { return f64_to_i64_x86(v); }
+  __device__ static inline double to_f64(int64_t v) { return (double)v; }
+  __device__ static inline int64_t diff(int64_t a, int64_t b) {
+    return (int64_t)((uint64_t)a - (uint64_t)b);
+  }
+};
+
+// ---- XCD-contiguous work mapping -----------------------------------------
+// Blocks are dealt round-robin over the 8 XCDs (blocks b and b+8 share an L2).
+// Each XCD gets one contiguous slice of the row-major work list, walked by its
+// blocks in order, so source rows fetched into that XCD's L2 are re-used by the
+// next target rows it processes.  Placement affects speed only.
+struct XcdSlice {
+  int64_t begin, end, step, first;
+};
+__device__ inline XcdSlice xcd_slice(int64_t nwork) {
+  const int64_t nxcd = 8;
+  const int64_t b = blockIdx.x, nb = gridDim.x;  // launcher: nb % 8 == 0
+  const int64_t xcd = b % nxcd, per = nb / nxcd, lane = b / nxcd;
+  const int64_t chunk = (nwork + nxcd - 1) / nxcd;
+  XcdSlice s;
+  s.begin = xcd * chunk;
+  s.end = s.begin + chunk < nwork ? s.begin + chunk : nwork;
+  s.step = per;
+  s.first = s.begin + lane;
+  return s;
+}
+
+template <typename F>
+inline int dispatch_dtype(int dtype, F&& f) {
+  switch (dtype) {
+    case XRS_DTYPE_U8: return f((uint8_t)0);
+    case XRS_DTYPE_I8: return f((int8_t)0);
+    case XRS_DTYPE_U16: return f((uint16_t)0);
+    case XRS_DTYPE_I16: return f((int16_t)0);
+    case XRS_DTYPE_U32: return f((uint32_t)0);
+    case XRS_DTYPE_I32: return f((int32_t)0);
+    case XRS_DTYPE_I64: return f((int64_t)0);
+    case XRS_DTYPE_F32: return f((float)0);
+    case XRS_DTYPE_F64: return f((double)0);
+    default: return XRS_ERR_ARG;
+  }
+}
+
+inline int grid_blocks(int64_t nwork, int per_block, int cap) {
+  int64_t nb = (nwork + per_block - 1) / per_block;
+  if (nb > cap) nb = cap;
+  nb = ((nb + 7) / 8) * 8;  // multiple of the XCD count
+  if (nb < 8) nb = 8;
+  return (int)nb;
+}
+
+}  // namespace xrs
+
+// Thread-local error message reported through xrs_last_error().
+void xrs_set_error(const char* fmt, ...);
+
+#define XRS_HIP_CHECK(expr)                                                    \
+  do {                                                                         \
+    hipError_t _e = (expr);                                                    \
+    if (_e != hipSuccess) {                                                    \
+      xrs_set_error("%s failed: %s", #expr, hipGetErrorString(_e));            \
+      return XRS_ERR_HIP;                                                      \
+    }                                                                          \
+  } while (0)

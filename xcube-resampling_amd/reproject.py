@@ -1,0 +1,263 @@
+"""Regular -> regular reprojection across CRSs (reference: reproject.py).
+
+Host side (this module) restates the reference's orchestration and tiling math
+— ``reproject_dataset`` (reproject.py:51-186), ``_reproject_data_array``
+(189-265), ``_downscale_source_dataset`` (338-382),
+``_get_scr_bboxes_indices`` (385-469) and ``_transform_gridpoints``
+(472-496) — and hands ALL target tiles of a variable to one launch of the K1
+HIP kernel (``xrs_reproject``), which replaces ``_reproject_block``
+(268-335) and the pad/copy of ``_reorganize_data_array_slice`` (499-530).
+
+Device data layout: the source variable lives in HBM as one contiguous
+(n, H, W) array (never reorganised into per-tile windows); the target is one
+(n, H', W') array.  The per-tile window geometry is a few small tables; the
+target pixel coordinates in the source CRS are two 1-D float64 tables
+(separable CRS pairs, e.g. EPSG:3857 -> EPSG:4326) instead of the reference's
+two materialised (H', W') float64 grids.
+"""
+
+from __future__ import annotations
+
+import math
+from collections.abc import Iterable
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import kernels
+from .constants import SCALE_LIMIT
+from .crs import Transformer
+from .dataset import DataArray, Dataset
+from .device import is_device_array, require_device, to_device, torch
+from .gridmapping import GridMapping
+from .options import get_options
+from .utils import (
+    _get_fill_value,
+    _get_interp_method_str,
+    _prep_interp_methods_downscale,
+    _select_variables,
+    as_dataset,
+    clip_dataset_by_bbox,
+    normalize_grid_mapping,
+)
+
+
+@dataclass
+class ReprojectPlan:
+    """Host-computed tiling geometry of one (source_gm, target_gm) pair."""
+
+    src_width: int
+    src_height: int
+    dst_width: int
+    dst_height: int
+    tile_width: int
+    tile_height: int
+    x_res: float
+    y_res: float
+    coord_mode: int              # 0: separable tables, 1: 2-D tables
+    src_x: np.ndarray            # (W',) or (H', W') float64, target pixel x in source CRS
+    src_y: np.ndarray            # (H',) or (H', W') float64
+    tile_x0: np.ndarray          # (ntiles,) float32, window x origin (reproject.py:427-453)
+    tile_y0: np.ndarray          # (ntiles,) float32
+    tile_win: np.ndarray         # (ntiles, 2) int64, window (i0, j0) in unpadded source indices
+    win_width: int
+    win_height: int
+    scr_ij_bboxes: np.ndarray    # (4, nty, ntx) int32, as returned by the reference (padded)
+    pad_width: tuple
+    _device_cache: dict = field(default_factory=dict, repr=False)
+
+    @property
+    def num_tiles(self) -> tuple[int, int]:
+        return self.scr_ij_bboxes.shape[2], self.scr_ij_bboxes.shape[1]
+
+    def device_tables(self, device) -> dict:
+        key = str(device)
+        tabs = self._device_cache.get(key)
+        if tabs is None:
+            tabs = dict(
+                src_x=to_device(np.ascontiguousarray(self.src_x, np.float64), device),
+                src_y=to_device(np.ascontiguousarray(self.src_y, np.float64), device),
+                tile_x0=to_device(self.tile_x0.astype(np.float32), device),
+                tile_y0=to_device(self.tile_y0.astype(np.float32), device),
+                tile_win=to_device(np.ascontiguousarray(self.tile_win, np.int64), device),
+            )
+            self._device_cache[key] = tabs
+        return tabs
+
+    def source_rows_for(self, r0: int, r1: int) -> tuple[int, int]:
+        """Global source rows [j0, j1) read by target rows [r0, r1) (clipped)."""
+        tys = range(r0 // self.tile_height, (max(r1, r0 + 1) - 1) // self.tile_height + 1)
+        ntx = self.num_tiles[0]
+        t = np.array([ty * ntx + tx for ty in tys for tx in range(ntx)], dtype=np.int64)
+        j0 = int(self.tile_win[t, 1].min())
+        j1 = int(self.tile_win[t, 1].max()) + self.win_height
+        return max(0, j0), min(self.src_height, max(0, j1))
+
+
+def plan_reproject(source_gm: GridMapping, target_gm: GridMapping,
+                   transformer: Transformer) -> ReprojectPlan:
+    """Restates reproject.py:385-469 and 472-496."""
+    num_tiles_x = math.ceil(target_gm.width / target_gm.tile_width)
+    num_tiles_y = math.ceil(target_gm.height / target_gm.tile_height)
+
+    origin = source_gm.x_coords.values[0], source_gm.y_coords.values[0]
+    bboxes = np.full((4, num_tiles_y, num_tiles_x), -1, dtype=np.int32)
+    for idx, xy_bbox in enumerate(target_gm.xy_bboxes):
+        j, i = np.unravel_index(idx, (num_tiles_y, num_tiles_x))
+        sb = transformer.transform_bounds(*xy_bbox)
+        bboxes[:, j, i] = [
+            math.floor((sb[0] - origin[0]) / source_gm.x_res),
+            math.floor((origin[1] - sb[3]) / source_gm.y_res),
+            math.ceil((sb[2] - origin[0]) / source_gm.x_res),
+            math.ceil((origin[1] - sb[1]) / source_gm.y_res),
+        ]
+
+    # uniform window size (reproject.py:405-423)
+    i_diff = bboxes[2] - bboxes[0]
+    j_diff = bboxes[3] - bboxes[1]
+    i_diff_max = np.max(i_diff) + 1
+    j_diff_max = np.max(j_diff) + 1
+    i_start = bboxes[0] - (i_diff_max - i_diff) // 2
+    j_start = bboxes[1] - (j_diff_max - j_diff) // 2
+    bboxes = np.stack([i_start, j_start, i_start + i_diff_max, j_start + j_diff_max]).astype(np.int32)
+
+    # window origins (reproject.py:427-450), float32 like the reference's x_coords
+    i_min = np.min(bboxes[0])
+    i_max = np.max(bboxes[2])
+    j_min = np.min(bboxes[[1, 3]])
+    j_max = np.max(bboxes[[1, 3]])
+    x0 = source_gm.x_coords.values[0]
+    x_coord = np.arange(x0 + i_min * source_gm.x_res, x0 + i_max * source_gm.x_res,
+                        source_gm.x_res)
+    yv = source_gm.y_coords.values
+    y_res = yv[1] - yv[0]
+    y_coord = np.arange(yv[0] + j_min * y_res, yv[0] + j_max * y_res, y_res)
+    tile_x0 = x_coord[(bboxes[0] - i_min).ravel()].astype(np.float32)
+    tile_y0 = y_coord[(bboxes[1] - j_min).ravel()].astype(np.float32)
+    tile_win = np.stack([bboxes[0].ravel(), bboxes[1].ravel()], axis=1).astype(np.int64)
+
+    pad_width = ((0, 0),
+                 (-min(0, int(j_min)), max(0, int(j_max - source_gm.height))),
+                 (-min(0, int(i_min)), max(0, int(i_max - source_gm.width))))
+    scr_ij_bboxes = bboxes.copy()
+    scr_ij_bboxes[[1, 3]] += pad_width[1][0]
+    scr_ij_bboxes[[0, 2]] += pad_width[2][0]
+
+    # target pixel centres in the source CRS (reproject.py:472-496)
+    tx = target_gm.x_coords.values
+    ty = target_gm.y_coords.values
+    if transformer.is_separable:
+        coord_mode = 0
+        src_x = transformer.transform_x(tx)
+        src_y = transformer.transform_y(ty)
+    else:
+        coord_mode = 1
+        xx, yy = np.meshgrid(tx, ty)
+        src_x, src_y = transformer.transform(xx, yy)
+
+    return ReprojectPlan(
+        src_width=source_gm.width, src_height=source_gm.height,
+        dst_width=target_gm.width, dst_height=target_gm.height,
+        tile_width=target_gm.tile_width, tile_height=target_gm.tile_height,
+        x_res=source_gm.x_res, y_res=source_gm.y_res, coord_mode=coord_mode,
+        src_x=np.asarray(src_x, np.float64), src_y=np.asarray(src_y, np.float64),
+        tile_x0=tile_x0, tile_y0=tile_y0, tile_win=tile_win,
+        win_width=int(i_diff_max), win_height=int(j_diff_max),
+        scr_ij_bboxes=scr_ij_bboxes, pad_width=pad_width,
+    )
+
+
+def reproject_dataset(source_ds, target_gm: GridMapping, source_gm: GridMapping | None = None,
+                      variables: str | Iterable[str] | None = None, interp_methods=None,
+                      agg_methods=None, recover_nans=False, fill_values=None) -> Dataset:
+    """Reproject a dataset to the CRS and grid of ``target_gm``
+    (reproject.py:51-186; same arguments, defaults and errors)."""
+    source_ds = as_dataset(source_ds)
+    if source_gm is None:
+        source_gm = GridMapping.from_dataset(source_ds)
+    if source_gm.is_j_axis_up:
+        v_var = source_gm.xy_var_names[1]
+        source_ds = source_ds.isel({v_var: slice(None, None, -1)})
+        source_gm = GridMapping.from_dataset(source_ds)
+
+    source_ds = normalize_grid_mapping(source_ds, source_gm)
+    source_ds = _select_variables(source_ds, variables)
+    transformer = Transformer.from_crs(target_gm.crs, source_gm.crs, always_xy=True)
+
+    source_ds, source_gm = _downscale_source_dataset(
+        source_ds, source_gm, target_gm, transformer, interp_methods, agg_methods, recover_nans)
+
+    plan = plan_reproject(source_gm, target_gm, transformer)
+
+    x_name, y_name = source_gm.xy_var_names
+    coords = {k: v for k, v in source_ds.coords.items() if k not in (x_name, y_name)}
+    tx_name, ty_name = target_gm.xy_var_names
+    coords[tx_name] = DataArray(target_gm.x_coords.values, target_gm.x_coords.dims)
+    coords[ty_name] = DataArray(target_gm.y_coords.values, target_gm.y_coords.dims)
+    coords["spatial_ref"] = DataArray(np.array(0), (), target_gm.crs.to_cf())
+    target_ds = Dataset(coords=coords, attrs=source_ds.attrs)
+
+    yx_dims = (source_gm.xy_dim_names[1], source_gm.xy_dim_names[0])
+    for var_name, data_array in source_ds.items():
+        if data_array.dims[-2:] == yx_dims:
+            assert len(data_array.dims) in (2, 3), \
+                f"Data variable {var_name} has {len(data_array.dims)} dimensions."
+            target_ds[var_name] = _reproject_data_array(
+                data_array, var_name, target_gm, plan, interp_methods, fill_values)
+        elif yx_dims[0] not in data_array.dims and yx_dims[1] not in data_array.dims:
+            target_ds[var_name] = data_array
+    return target_ds
+
+
+def _reproject_data_array(data_array: DataArray, var_name, target_gm: GridMapping,
+                          plan: ReprojectPlan, interp_methods, fill_values) -> DataArray:
+    """reproject.py:189-265 — one kernel launch over all tiles and dim-0 slices."""
+    fill_value = _get_fill_value(fill_values, var_name, data_array)
+    interp_method = _get_interp_method_str(interp_methods, var_name, data_array)
+    device = require_device()
+    data = data_array.data
+    on_device = is_device_array(data)
+    src = to_device(data, device)
+    expanded = src.dim() == 2
+    if expanded:
+        src = src.unsqueeze(0)
+    out_dtype = None
+    if interp_method == "bilinear" and get_options()["reproject_bilinear_dtype"] == "source":
+        out_dtype = data_array.dtype if np.issubdtype(data_array.dtype, np.floating) else np.float64
+    out = kernels.reproject(src, plan, interp_method, fill_value, out_dtype=out_dtype)
+    if expanded:
+        out = out[0]
+        dims = (target_gm.xy_dim_names[1], target_gm.xy_dim_names[0])
+    else:
+        dims = (data_array.dims[0], target_gm.xy_dim_names[1], target_gm.xy_dim_names[0])
+    result = out if on_device else out.cpu().numpy()
+    return DataArray(result, dims, data_array.attrs)
+
+
+def _downscale_source_dataset(source_ds, source_gm: GridMapping, target_gm: GridMapping,
+                              transformer: Transformer, interp_methods, agg_methods,
+                              recover_nans):
+    """reproject.py:338-382 — pre-downscale a finer source with the affine path."""
+    bbox_trans = transformer.transform_bounds(*target_gm.xy_bbox)
+    xres_trans = (bbox_trans[2] - bbox_trans[0]) / target_gm.width
+    yres_trans = (bbox_trans[3] - bbox_trans[1]) / target_gm.height
+    x_scale = source_gm.x_res / xres_trans
+    y_scale = source_gm.y_res / yres_trans
+    if x_scale < SCALE_LIMIT or y_scale < SCALE_LIMIT:
+        from .affine import affine_transform_dataset
+
+        bbox_trans = (bbox_trans[0] - 2 * source_gm.x_res, bbox_trans[1] - 2 * source_gm.y_res,
+                      bbox_trans[2] + 2 * source_gm.x_res, bbox_trans[3] + 2 * source_gm.y_res)
+        source_ds = clip_dataset_by_bbox(source_ds, bbox_trans, source_gm.xy_dim_names)
+        source_gm = GridMapping.from_dataset(source_ds)
+        w, h = round(x_scale * source_gm.width), round(y_scale * source_gm.height)
+        downscaled_size = (w if w >= 2 else 2, h if h >= 2 else 2)
+        downscale_target_gm = GridMapping.regular(
+            size=downscaled_size, xy_min=(source_gm.xy_bbox[0], source_gm.xy_bbox[1]),
+            xy_res=(xres_trans, yres_trans), crs=source_gm.crs, tile_size=source_gm.tile_size)
+        source_ds = affine_transform_dataset(
+            source_ds, downscale_target_gm, source_gm=source_gm,
+            interp_methods=_prep_interp_methods_downscale(interp_methods),
+            agg_methods=agg_methods, recover_nans=recover_nans)
+        source_gm = GridMapping.from_dataset(source_ds)
+    return source_ds, source_gm
