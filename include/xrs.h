@@ -92,7 +92,12 @@ const char* xrs_last_error(void);
  *      ntiles = ceil(dst_h/tile_h) * ceil(dst_w/tile_w), row-major.
  * dst_dtype: = src_dtype for nearest/triangular; float32 or float64 for
  *      bilinear (the reference yields float64 there; float32 = declared dtype).
+ * workspace: device scratch of xrs_reproject_workspace_size(...) bytes (the
+ *      per-(tile, column) / (tile, row) index tables of coord_mode 0).
  * ------------------------------------------------------------------------- */
+int64_t xrs_reproject_workspace_size(int64_t dst_h, int64_t dst_w, int64_t tile_h,
+                                     int64_t tile_w, int coord_mode);
+
 int xrs_reproject(const void* src, int src_dtype, int64_t n, int64_t src_h,
                   int64_t src_w, int64_t src_row0, int64_t src_rows,
                   int64_t src_sn, int64_t src_sy, void* dst, int dst_dtype,
@@ -102,7 +107,8 @@ int xrs_reproject(const void* src, int src_dtype, int64_t n, int64_t src_h,
                   const double* src_y, int coord_mode, const float* tile_x0,
                   const float* tile_y0, const int64_t* tile_win,
                   int64_t win_h, int64_t win_w, double x_res, double y_res,
-                  int interp, double fill, int32_t* err_flags, void* stream);
+                  int interp, double fill, void* workspace,
+                  int64_t workspace_bytes, int32_t* err_flags, void* stream);
 
 #ifdef __cplusplus
 }

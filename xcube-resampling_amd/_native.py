@@ -64,8 +64,10 @@ _SIGNATURES = {
         _c_i64, _c_i64,                                                          # tile
         _c_ptr, _c_ptr, _c_int,                                                  # coords
         _c_ptr, _c_ptr, _c_ptr, _c_i64, _c_i64,                                  # tile tables
-        _c_dbl, _c_dbl, _c_int, _c_dbl, _c_ptr, _c_ptr,                          # res, interp...
+        _c_dbl, _c_dbl, _c_int, _c_dbl,                                          # res, interp, fill
+        _c_ptr, _c_i64, _c_ptr, _c_ptr,                                          # ws, flags, stream
     ]),
+    "xrs_reproject_workspace_size": (_c_i64, [_c_i64, _c_i64, _c_i64, _c_i64, _c_int]),
 }
 
 _lib = None

@@ -1,18 +1,33 @@
 // xrs_reproject.hip — K1: regular->regular reprojection gather for gfx950.
 //
-// Replaces, for all target tiles of one variable in ONE launch:
+// Replaces, for all target tiles of one variable in ONE call:
 //   * reproject._reproject_block            (reproject.py:268-335)  per-tile gather/lerp
 //   * reproject._reorganize_data_array_slice (reproject.py:499-530)  pad + window copy
 // The per-tile window geometry (reproject._get_scr_bboxes_indices,
-// reproject.py:385-469) is computed by the host and passed as tables.
+// reproject.py:385-469) is computed by the host and passed as small tables.
 //
-// Memory-bound gather: one thread = 4 consecutive target pixels of one row;
-// one workgroup = 1024 pixels of one row; each XCD walks a contiguous band of
-// rows so the source rows it pulls into its 4 MiB L2 serve the next target rows
-// (scale ~1 => every source row is read by ~2 target rows).  Output stores are
-// 16-byte vectors where aligned.  Index math is float64 without contraction
-// (library built with -ffp-contract=off) so nearest-neighbour picks and lerp
-// weights are bit-identical to numpy's.
+// Separable CRS pairs (coord_mode 0: target x -> source x only, y -> y only,
+// e.g. EPSG:3857 -> EPSG:4326) run in two launches:
+//   K1a axis_tables   : for every (tile, column) and (tile, row) resolve the
+//                       reference's per-pixel index math ONCE — ix = (sx-x0)/res,
+//                       floor/ceil/rint, int16 cast, python-style window wrap,
+//                       window -> source index, pad -> "outside" — into
+//                       {idx_floor, idx_ceil, frac} entries (16 B).  Bit-exact
+//                       because for separable transforms the per-pixel ix only
+//                       depends on the column (iy on the row).
+//   K1b gather_sep    : the HBM-bound part.  One work item = one tile x one
+//                       1024-column segment x one band of kBand rows, so the tile
+//                       (and every row entry) is block-uniform: row pointers are
+//                       scalar, lane offsets 32-bit.  Lanes take consecutive
+//                       columns (each wave-load touches ~256 contiguous source
+//                       bytes, each store writes 256 contiguous bytes); source
+//                       rows are carried in registers from one target row to the
+//                       next (scale ~1: each source row is loaded once per band).
+// Non-separable pairs (coord_mode 1: 2-D coordinate tables) run K1c, the same
+// work decomposition with the index math done per pixel.
+//
+// Index and weight math is float64 without contraction (-ffp-contract=off) so
+// nearest picks and lerp weights are bit-identical to numpy's.
 
 #include "xrs_common.hpp"
 
@@ -20,15 +35,21 @@ namespace xrs {
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int kPx = 4;                      // pixels per thread (one row)
-constexpr int kBlockPx = kThreads * kPx;    // pixels per work item
+constexpr int kPx = 4;                       // columns per thread
+constexpr int kSegW = kThreads * kPx;        // columns per work item
+constexpr int kBand = 32;                    // target rows per work item
 
-struct ReprojectArgs {
-  const void* src;
-  int64_t n, src_h, src_w, src_row0, src_rows, src_sn, src_sy;
-  void* dst;
-  int64_t dst_h, dst_w, row_begin, row_end, dst_sn, dst_sy;
-  int64_t tile_h, tile_w, ntiles_x;
+struct AxisEntry {   // one resolved column (or row) of one tile
+  int32_t f;         // source index of floor(ix) (nearest: of rint(ix)); -1 = outside source
+  int32_t c;         // source index of ceil(ix); -1 = outside source
+  double d;          // ix - (double)(int16)floor(ix)
+};
+static_assert(sizeof(AxisEntry) == 16, "AxisEntry layout");
+
+struct Geometry {
+  int64_t src_h, src_w, src_row0, src_rows;
+  int64_t dst_h, dst_w, row_begin, row_end;
+  int64_t tile_h, tile_w, ntiles_x, ntiles_y;
   const double* src_x;
   const double* src_y;
   const float* tile_x0;
@@ -36,7 +57,6 @@ struct ReprojectArgs {
   const int64_t* tile_win;
   int64_t win_h, win_w;
   double x_res, neg_y_res;
-  double fill;
   int32_t* err_flags;
 };
 
@@ -50,171 +70,322 @@ __device__ inline bool window_index(int16_t idx16, int64_t win, int64_t& out) {
   return i >= 0 && i < win;
 }
 
-// A tap offset < 0 means "outside the source" -> the da.pad constant fill.
-template <typename T>
-__device__ inline T fetch(const T* __restrict__ src, int64_t off, int64_t slice_off, T fill) {
-  return off >= 0 ? src[slice_off + off] : fill;
-}
-
-template <typename O>
-__device__ inline void store_px(O* __restrict__ row, int64_t c0, int nvalid, const O (&v)[kPx]) {
-#pragma unroll
-  for (int k = 0; k < kPx; ++k)
-    if (k < nvalid) row[c0 + k] = v[k];
-}
-template <>
-__device__ inline void store_px<float>(float* __restrict__ row, int64_t c0, int nvalid,
-                                       const float (&v)[kPx]) {
-  float* p = row + c0;
-  if (nvalid == kPx && (((uintptr_t)p) & 15) == 0) {
-    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
-  } else {
-#pragma unroll
-    for (int k = 0; k < kPx; ++k)
-      if (k < nvalid) p[k] = v[k];
-  }
-}
-template <>
-__device__ inline void store_px<double>(double* __restrict__ row, int64_t c0, int nvalid,
-                                        const double (&v)[kPx]) {
-  double* p = row + c0;
-  if (nvalid == kPx && (((uintptr_t)p) & 15) == 0) {
-    reinterpret_cast<double2*>(p)[0] = make_double2(v[0], v[1]);
-    reinterpret_cast<double2*>(p)[1] = make_double2(v[2], v[3]);
-  } else {
-#pragma unroll
-    for (int k = 0; k < kPx; ++k)
-      if (k < nvalid) p[k] = v[k];
-  }
-}
-
-// Resolve window indices (wy, wx) of tile t to a source offset within a slice.
-__device__ inline int64_t resolve(const ReprojectArgs& a, int64_t j0, int64_t i0,
-                                  int64_t wy, int64_t wx, int32_t& eflags) {
-  const int64_t gj = j0 + wy, gi = i0 + wx;
-  if (gj < 0 || gj >= a.src_h || gi < 0 || gi >= a.src_w) return -1;  // pad region
-  const int64_t lj = gj - a.src_row0;
-  if (lj < 0 || lj >= a.src_rows) {  // host plan did not give this device the band
+// Window position -> source index along one axis; -1 when the window position
+// lies in the constant-padded region (outside the source).  Rows are returned
+// relative to the band held on this device.
+__device__ inline int32_t to_source(int64_t w0, int64_t widx, int64_t size, int64_t band0,
+                                    int64_t band_len, int32_t& eflags) {
+  const int64_t g = w0 + widx;
+  if (g < 0 || g >= size) return -1;
+  const int64_t l = g - band0;
+  if (l < 0 || l >= band_len) {
     eflags |= XRS_EFLAG_BAND;
     return -1;
   }
-  return lj * a.src_sy + gi;
+  return (int32_t)l;
 }
 
-template <typename T, typename O, int INTERP, int COORD>
-__global__ void __launch_bounds__(kThreads)
-reproject_kernel(ReprojectArgs a) {
-  const T* __restrict__ src = static_cast<const T*>(a.src);
-  O* __restrict__ dst = static_cast<O*>(a.dst);
-  const T fill = Conv<T>::from_f64(a.fill);
-  const int64_t nrows = a.row_end - a.row_begin;
-  const int64_t nbcol = (a.dst_w + kBlockPx - 1) / kBlockPx;
-  const XcdSlice s = xcd_slice(nrows * nbcol);
-  int32_t eflags = 0;
-
-  for (int64_t w = s.first; w < s.end; w += s.step) {
-    const int64_t lr = w / nbcol;            // local target row
-    const int64_t r = a.row_begin + lr;      // global target row
-    const int64_t c0 = (w - lr * nbcol) * kBlockPx + (int64_t)threadIdx.x * kPx;
-    if (c0 >= a.dst_w) continue;
-    const int nvalid = (int)min((int64_t)kPx, a.dst_w - c0);
-    const int64_t ty = r / a.tile_h;
-
-    // ---- per-pixel geometry (independent of the slice index n) ----------
-    int64_t off[kPx][4];
-    double dx[kPx], dy[kPx];
-#pragma unroll
-    for (int k = 0; k < kPx; ++k) {
-      off[k][0] = off[k][1] = off[k][2] = off[k][3] = -1;
-      dx[k] = dy[k] = 0.0;
-      if (k >= nvalid) continue;
-      const int64_t c = c0 + k;
-      const int64_t t = ty * a.ntiles_x + c / a.tile_w;
-      double sx, sy;
-      if (COORD == 0) {
-        sx = a.src_x[c];
-        sy = a.src_y[r];
-      } else {
-        sx = a.src_x[r * a.dst_w + c];
-        sy = a.src_y[r * a.dst_w + c];
-      }
-      const double ix = (sx - (double)a.tile_x0[t]) / a.x_res;      // reproject.py:278
-      const double iy = (sy - (double)a.tile_y0[t]) / a.neg_y_res;  // reproject.py:279
-      const int64_t wi0 = a.tile_win[2 * t], wj0 = a.tile_win[2 * t + 1];
-      if (INTERP == XRS_INTERP_NEAREST) {                            // reproject.py:281-284
-        int64_t wx, wy;
-        const bool okx = window_index(f64_to_i16_np(rint(ix)), a.win_w, wx);
-        const bool oky = window_index(f64_to_i16_np(rint(iy)), a.win_h, wy);
-        if (okx && oky) off[k][0] = resolve(a, wj0, wi0, wy, wx, eflags);
-        else eflags |= XRS_EFLAG_INDEX;
-      } else {                                                       // reproject.py:286-289,316-321
-        const int16_t ixc = f64_to_i16_np(ceil(ix)), ixf = f64_to_i16_np(floor(ix));
-        const int16_t iyc = f64_to_i16_np(ceil(iy)), iyf = f64_to_i16_np(floor(iy));
-        dx[k] = ix - (double)ixf;
-        dy[k] = iy - (double)iyf;
-        int64_t wxf, wxc, wyf, wyc;
-        // all four resolved (no short-circuit): each IndexError is flagged
-        const int ok = (int)window_index(ixf, a.win_w, wxf) & (int)window_index(ixc, a.win_w, wxc) &
-                       (int)window_index(iyf, a.win_h, wyf) & (int)window_index(iyc, a.win_h, wyc);
-        if (ok) {
-          off[k][0] = resolve(a, wj0, wi0, wyf, wxf, eflags);  // value_00
-          off[k][1] = resolve(a, wj0, wi0, wyf, wxc, eflags);  // value_01
-          off[k][2] = resolve(a, wj0, wi0, wyc, wxf, eflags);  // value_10
-          off[k][3] = resolve(a, wj0, wi0, wyc, wxc, eflags);  // value_11
-        } else {
-          eflags |= XRS_EFLAG_INDEX;
-        }
-      }
+// The reference's index math for one coordinate along one axis
+// (reproject.py:278-283 nearest, 286-291 / 316-321 floor/ceil/diff).
+template <int INTERP>
+__device__ inline AxisEntry resolve_axis(double coord, float origin, double res, int64_t win,
+                                         int64_t w0, int64_t size, int64_t band0,
+                                         int64_t band_len, int32_t& eflags) {
+  const double i = (coord - (double)origin) / res;
+  AxisEntry e;
+  if (INTERP == XRS_INTERP_NEAREST) {
+    int64_t wi;
+    if (window_index(f64_to_i16_np(rint(i)), win, wi)) {
+      e.f = to_source(w0, wi, size, band0, band_len, eflags);
+    } else {
+      eflags |= XRS_EFLAG_INDEX;
+      e.f = -1;
     }
+    e.c = e.f;
+    e.d = 0.0;
+  } else {
+    const int16_t fi = f64_to_i16_np(floor(i)), ci = f64_to_i16_np(ceil(i));
+    e.d = i - (double)fi;
+    int64_t wf, wc;
+    const bool okf = window_index(fi, win, wf);
+    const bool okc = window_index(ci, win, wc);
+    if (!okf || !okc) eflags |= XRS_EFLAG_INDEX;
+    e.f = okf ? to_source(w0, wf, size, band0, band_len, eflags) : -1;
+    e.c = okc ? to_source(w0, wc, size, band0, band_len, eflags) : -1;
+  }
+  return e;
+}
 
-    // ---- gather + interpolate every slice of dim 0 ----------------------
-    for (int64_t sn = 0; sn < a.n; ++sn) {
-      const int64_t so = sn * a.src_sn;
-      O out[kPx];
-#pragma unroll
-      for (int k = 0; k < kPx; ++k) {
-        if (INTERP == XRS_INTERP_NEAREST) {
-          out[k] = (O)fetch(src, off[k][0], so, fill);
-        } else {
-          const T v00 = fetch(src, off[k][0], so, fill);
-          const T v01 = fetch(src, off[k][1], so, fill);
-          const T v10 = fetch(src, off[k][2], so, fill);
-          const T v11 = fetch(src, off[k][3], so, fill);
-          double res;
-          if (INTERP == XRS_INTERP_BILINEAR) {               // reproject.py:326-328
-            const double u0 = Conv<T>::to_f64(v00) + dx[k] * Conv<T>::to_f64(Conv<T>::diff(v01, v00));
-            const double u1 = Conv<T>::to_f64(v10) + dx[k] * Conv<T>::to_f64(Conv<T>::diff(v11, v10));
-            res = u0 + dy[k] * (u1 - u0);
-          } else if (dx[k] + dy[k] < 1.0) {                   // reproject.py:296,304-308
-            res = Conv<T>::to_f64(v00) + dx[k] * Conv<T>::to_f64(Conv<T>::diff(v01, v00)) +
-                  dy[k] * Conv<T>::to_f64(Conv<T>::diff(v10, v00));
-          } else {                                            // reproject.py:310-314
-            res = Conv<T>::to_f64(v11) + (1.0 - dx[k]) * Conv<T>::to_f64(Conv<T>::diff(v10, v11)) +
-                  (1.0 - dy[k]) * Conv<T>::to_f64(Conv<T>::diff(v01, v11));
-          }
-          out[k] = Conv<O>::from_f64(res);
-        }
-      }
-      store_px<O>(dst + sn * a.dst_sn + lr * a.dst_sy, c0, nvalid, out);
+// ---- K1a: axis tables ------------------------------------------------------
+template <int INTERP>
+__global__ void __launch_bounds__(kThreads)
+axis_tables_kernel(Geometry g, AxisEntry* __restrict__ xtab, AxisEntry* __restrict__ ytab) {
+  const int64_t ntiles = g.ntiles_x * g.ntiles_y;
+  const int64_t nx = ntiles * g.tile_w, total = nx + ntiles * g.tile_h;
+  int32_t eflags = 0;
+  for (int64_t idx = (int64_t)blockIdx.x * kThreads + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * kThreads) {
+    if (idx < nx) {
+      const int64_t t = idx / g.tile_w, k = idx - t * g.tile_w;
+      const int64_t c = (t % g.ntiles_x) * g.tile_w + k;
+      const int64_t r0 = (t / g.ntiles_x) * g.tile_h;
+      AxisEntry e{-1, -1, 0.0};
+      // tiles outside the computed rows [row_begin, row_end) are never read
+      if (c < g.dst_w && r0 < g.row_end && r0 + g.tile_h > g.row_begin)
+        e = resolve_axis<INTERP>(g.src_x[c], g.tile_x0[t], g.x_res, g.win_w, g.tile_win[2 * t],
+                                 g.src_w, 0, g.src_w, eflags);
+      xtab[idx] = e;
+    } else {
+      const int64_t j = idx - nx;
+      const int64_t t = j / g.tile_h, k = j - t * g.tile_h;
+      const int64_t r = (t / g.ntiles_x) * g.tile_h + k;
+      AxisEntry e{-1, -1, 0.0};
+      if (r >= g.row_begin && r < g.row_end)
+        e = resolve_axis<INTERP>(g.src_y[r], g.tile_y0[t], g.neg_y_res, g.win_h,
+                                 g.tile_win[2 * t + 1], g.src_h, g.src_row0, g.src_rows, eflags);
+      ytab[j] = e;
     }
   }
-  if (eflags) atomicOr(a.err_flags, eflags);
+  if (eflags) atomicOr(g.err_flags, eflags);
+}
+
+// ---- interpolation of one pixel (reproject.py:304-314, 326-328) ------------
+template <typename T, int INTERP>
+__device__ inline double interp4(T v00, T v01, T v10, T v11, double dx, double dy) {
+  if (INTERP == XRS_INTERP_BILINEAR) {
+    const double u0 = Conv<T>::to_f64(v00) + dx * Conv<T>::to_f64(Conv<T>::diff(v01, v00));
+    const double u1 = Conv<T>::to_f64(v10) + dx * Conv<T>::to_f64(Conv<T>::diff(v11, v10));
+    return u0 + dy * (u1 - u0);
+  }
+  if (dx + dy < 1.0)  // closest triangle
+    return Conv<T>::to_f64(v00) + dx * Conv<T>::to_f64(Conv<T>::diff(v01, v00)) +
+           dy * Conv<T>::to_f64(Conv<T>::diff(v10, v00));
+  return Conv<T>::to_f64(v11) + (1.0 - dx) * Conv<T>::to_f64(Conv<T>::diff(v10, v11)) +
+         (1.0 - dy) * Conv<T>::to_f64(Conv<T>::diff(v01, v11));
+}
+
+struct GatherArgs {
+  Geometry g;
+  const void* src;
+  int64_t n, src_sn, src_sy;
+  void* dst;
+  int64_t dst_sn, dst_sy;
+  double fill;
+  const AxisEntry* xtab;
+  const AxisEntry* ytab;
+};
+
+// Work decomposition shared by K1b/K1c: bands of kBand rows inside one tile row
+// x segments of kSegW columns inside one tile column.  Returns false for empty
+// items (partial edge tiles, rows outside [row_begin, row_end)).
+struct WorkItem {
+  int64_t t, ty, tx, r0, r1, c0, c1;
+};
+__device__ inline bool work_item(const Geometry& g, int64_t w, int64_t ty0, int64_t nsegs,
+                                 int64_t bands_per_tile, int64_t segs_per_tile, WorkItem& it) {
+  const int64_t b = w / nsegs, s = w - b * nsegs;
+  const int64_t tyi = b / bands_per_tile;
+  it.ty = ty0 + tyi;
+  const int64_t bi = b - tyi * bands_per_tile;
+  const int64_t tr0 = it.ty * g.tile_h;
+  it.r0 = max(g.row_begin, tr0 + bi * kBand);
+  it.r1 = min(min(g.row_end, tr0 + g.tile_h), tr0 + bi * kBand + kBand);
+  it.tx = s / segs_per_tile;
+  const int64_t si = s - it.tx * segs_per_tile;
+  it.c0 = it.tx * g.tile_w + si * kSegW;
+  it.c1 = min(min(g.dst_w, it.tx * g.tile_w + g.tile_w), it.c0 + kSegW);
+  it.t = it.ty * g.ntiles_x + it.tx;
+  return it.r0 < it.r1 && it.c0 < it.c1;
+}
+
+// ---- K1b: separable gather --------------------------------------------------
+template <typename T, typename O, int INTERP>
+__global__ void __launch_bounds__(kThreads)
+gather_separable_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t bands_per_tile,
+                        int64_t segs_per_tile, int64_t nwork) {
+  const Geometry& g = a.g;
+  const T fill = Conv<T>::from_f64(a.fill);
+  const XcdSlice sl = xcd_slice(nwork);
+  for (int64_t w = sl.first; w < sl.end; w += sl.step) {
+    WorkItem it;
+    if (!work_item(g, w, ty0, nsegs, bands_per_tile, segs_per_tile, it)) continue;
+
+    // per-lane columns: entries resolved by K1a
+    const AxisEntry* xt = a.xtab + it.t * g.tile_w + (it.c0 - it.tx * g.tile_w);
+    const int ncols = (int)(it.c1 - it.c0);
+    int32_t cf[kPx], cc[kPx];
+    double dx[kPx];
+#pragma unroll
+    for (int k = 0; k < kPx; ++k) {
+      const int lc = (int)threadIdx.x + k * kThreads;
+      AxisEntry e{-1, -1, 0.0};
+      if (lc < ncols) e = xt[lc];
+      cf[k] = e.f;
+      cc[k] = e.c;
+      dx[k] = e.d;
+    }
+    const AxisEntry* yt = a.ytab + it.t * g.tile_h - it.ty * g.tile_h;
+
+    for (int64_t sn = 0; sn < a.n; ++sn) {
+      const T* __restrict__ src = static_cast<const T*>(a.src) + sn * a.src_sn;
+      O* __restrict__ dst = static_cast<O*>(a.dst) + sn * a.dst_sn - g.row_begin * a.dst_sy + it.c0;
+      // source rows carried from one target row to the next
+      T vf0[kPx], vf1[kPx], vc0[kPx], vc1[kPx];
+      int32_t rowf = INT32_MIN, rowc = INT32_MIN;
+#pragma unroll
+      for (int k = 0; k < kPx; ++k) vf0[k] = vf1[k] = vc0[k] = vc1[k] = fill;
+
+      for (int64_t r = it.r0; r < it.r1; ++r) {
+        const AxisEntry ye = yt[r];  // block-uniform
+        T nf0[kPx], nf1[kPx];
+        // ---- floor row
+        if (ye.f == rowf) {
+#pragma unroll
+          for (int k = 0; k < kPx; ++k) { nf0[k] = vf0[k]; nf1[k] = vf1[k]; }
+        } else if (ye.f == rowc) {
+#pragma unroll
+          for (int k = 0; k < kPx; ++k) { nf0[k] = vc0[k]; nf1[k] = vc1[k]; }
+        } else if (ye.f < 0) {
+#pragma unroll
+          for (int k = 0; k < kPx; ++k) { nf0[k] = fill; nf1[k] = fill; }
+        } else {
+          const T* row = src + (int64_t)ye.f * a.src_sy;
+#pragma unroll
+          for (int k = 0; k < kPx; ++k) {
+            nf0[k] = cf[k] >= 0 ? row[max(cf[k], 0)] : fill;
+            nf1[k] = fill;
+            if (INTERP != XRS_INTERP_NEAREST) nf1[k] = cc[k] >= 0 ? row[max(cc[k], 0)] : fill;
+          }
+        }
+        if (INTERP == XRS_INTERP_NEAREST) {
+#pragma unroll
+          for (int k = 0; k < kPx; ++k) {
+            const int lc = (int)threadIdx.x + k * kThreads;
+            if (lc < ncols) dst[r * a.dst_sy + lc] = (O)nf0[k];
+            vf0[k] = nf0[k];
+          }
+          rowf = ye.f;
+          continue;
+        }
+        // ---- ceil row
+        T nc0[kPx], nc1[kPx];
+        if (ye.c == ye.f) {
+#pragma unroll
+          for (int k = 0; k < kPx; ++k) { nc0[k] = nf0[k]; nc1[k] = nf1[k]; }
+        } else if (ye.c == rowc) {
+#pragma unroll
+          for (int k = 0; k < kPx; ++k) { nc0[k] = vc0[k]; nc1[k] = vc1[k]; }
+        } else if (ye.c == rowf) {
+#pragma unroll
+          for (int k = 0; k < kPx; ++k) { nc0[k] = vf0[k]; nc1[k] = vf1[k]; }
+        } else if (ye.c < 0) {
+#pragma unroll
+          for (int k = 0; k < kPx; ++k) { nc0[k] = fill; nc1[k] = fill; }
+        } else {
+          const T* row = src + (int64_t)ye.c * a.src_sy;
+#pragma unroll
+          for (int k = 0; k < kPx; ++k) {
+            nc0[k] = cf[k] >= 0 ? row[max(cf[k], 0)] : fill;
+            nc1[k] = cc[k] >= 0 ? row[max(cc[k], 0)] : fill;
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < kPx; ++k) {
+          const int lc = (int)threadIdx.x + k * kThreads;
+          const double v = interp4<T, INTERP>(nf0[k], nf1[k], nc0[k], nc1[k], dx[k], ye.d);
+          if (lc < ncols) dst[r * a.dst_sy + lc] = Conv<O>::from_f64(v);
+          vf0[k] = nf0[k]; vf1[k] = nf1[k]; vc0[k] = nc0[k]; vc1[k] = nc1[k];
+        }
+        rowf = ye.f;
+        rowc = ye.c;
+      }
+    }
+  }
+}
+
+// ---- K1c: per-pixel gather (2-D coordinate tables) --------------------------
+template <typename T, typename O, int INTERP>
+__global__ void __launch_bounds__(kThreads)
+gather_2d_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t bands_per_tile,
+                 int64_t segs_per_tile, int64_t nwork) {
+  const Geometry& g = a.g;
+  const T fill = Conv<T>::from_f64(a.fill);
+  const XcdSlice sl = xcd_slice(nwork);
+  int32_t eflags = 0;
+  for (int64_t w = sl.first; w < sl.end; w += sl.step) {
+    WorkItem it;
+    if (!work_item(g, w, ty0, nsegs, bands_per_tile, segs_per_tile, it)) continue;
+    const int ncols = (int)(it.c1 - it.c0);
+    const float x0 = g.tile_x0[it.t], y0 = g.tile_y0[it.t];
+    const int64_t wi0 = g.tile_win[2 * it.t], wj0 = g.tile_win[2 * it.t + 1];
+    for (int64_t r = it.r0; r < it.r1; ++r) {
+#pragma unroll
+      for (int k = 0; k < kPx; ++k) {
+        const int lc = (int)threadIdx.x + k * kThreads;
+        if (lc >= ncols) continue;
+        const int64_t p = r * g.dst_w + it.c0 + lc;
+        const AxisEntry ex = resolve_axis<INTERP>(g.src_x[p], x0, g.x_res, g.win_w, wi0, g.src_w,
+                                                  0, g.src_w, eflags);
+        const AxisEntry ey = resolve_axis<INTERP>(g.src_y[p], y0, g.neg_y_res, g.win_h, wj0,
+                                                  g.src_h, g.src_row0, g.src_rows, eflags);
+        for (int64_t sn = 0; sn < a.n; ++sn) {
+          const T* src = static_cast<const T*>(a.src) + sn * a.src_sn;
+          O* dst = static_cast<O*>(a.dst) + sn * a.dst_sn + (r - g.row_begin) * a.dst_sy;
+          auto at = [&](int32_t row, int32_t col) -> T {
+            return (row >= 0 && col >= 0) ? src[(int64_t)row * a.src_sy + col] : fill;
+          };
+          if (INTERP == XRS_INTERP_NEAREST) {
+            dst[it.c0 + lc] = (O)at(ey.f, ex.f);
+          } else {
+            const double v = interp4<T, INTERP>(at(ey.f, ex.f), at(ey.f, ex.c), at(ey.c, ex.f),
+                                                at(ey.c, ex.c), ex.d, ey.d);
+            dst[it.c0 + lc] = Conv<O>::from_f64(v);
+          }
+        }
+      }
+    }
+  }
+  if (eflags) atomicOr(g.err_flags, eflags);
 }
 
 template <typename T, typename O, int INTERP>
-int launch_coord(const ReprojectArgs& a, int coord_mode, hipStream_t stream) {
-  const int64_t nwork = (a.row_end - a.row_begin) * ((a.dst_w + kBlockPx - 1) / kBlockPx);
-  const int nb = grid_blocks(nwork, 1, 256 * 16);
-  if (coord_mode == 0)
-    hipLaunchKernelGGL((reproject_kernel<T, O, INTERP, 0>), dim3(nb), dim3(kThreads), 0, stream, a);
-  else
-    hipLaunchKernelGGL((reproject_kernel<T, O, INTERP, 1>), dim3(nb), dim3(kThreads), 0, stream, a);
+int launch(const GatherArgs& a, int coord_mode, AxisEntry* xtab, AxisEntry* ytab,
+           hipStream_t stream) {
+  const Geometry& g = a.g;
+  const int64_t ty0 = g.row_begin / g.tile_h, ty1 = (g.row_end - 1) / g.tile_h + 1;
+  const int64_t bands_per_tile = (g.tile_h + kBand - 1) / kBand;
+  const int64_t segs_per_tile = (g.tile_w + kSegW - 1) / kSegW;
+  const int64_t nsegs = g.ntiles_x * segs_per_tile;
+  const int64_t nwork = (ty1 - ty0) * bands_per_tile * nsegs;
+  const int nb = grid_blocks(nwork, 1, 256 * 8);
+  GatherArgs args = a;
+  if (coord_mode == 0) {
+    const int64_t ntab = g.ntiles_x * g.ntiles_y * (g.tile_w + g.tile_h);
+    const int nbt = grid_blocks(ntab, kThreads, 256 * 8);
+    hipLaunchKernelGGL((axis_tables_kernel<INTERP>), dim3(nbt), dim3(kThreads), 0, stream, g,
+                       xtab, ytab);
+    XRS_HIP_CHECK(hipGetLastError());
+    args.xtab = xtab;
+    args.ytab = ytab;
+    hipLaunchKernelGGL((gather_separable_kernel<T, O, INTERP>), dim3(nb), dim3(kThreads), 0,
+                       stream, args, ty0, nsegs, bands_per_tile, segs_per_tile, nwork);
+  } else {
+    hipLaunchKernelGGL((gather_2d_kernel<T, O, INTERP>), dim3(nb), dim3(kThreads), 0, stream,
+                       args, ty0, nsegs, bands_per_tile, segs_per_tile, nwork);
+  }
   XRS_HIP_CHECK(hipGetLastError());
   return XRS_OK;
 }
 
 }  // namespace
 }  // namespace xrs
+
+extern "C" int64_t xrs_reproject_workspace_size(int64_t dst_h, int64_t dst_w, int64_t tile_h,
+                                                int64_t tile_w, int coord_mode) {
+  if (coord_mode != 0 || dst_h < 1 || dst_w < 1 || tile_h < 1 || tile_w < 1) return 0;
+  const int64_t ntiles = ((dst_h + tile_h - 1) / tile_h) * ((dst_w + tile_w - 1) / tile_w);
+  return ntiles * (tile_w + tile_h) * (int64_t)sizeof(xrs::AxisEntry);
+}
 
 extern "C" int xrs_reproject(const void* src, int src_dtype, int64_t n, int64_t src_h,
                              int64_t src_w, int64_t src_row0, int64_t src_rows,
@@ -225,7 +396,8 @@ extern "C" int xrs_reproject(const void* src, int src_dtype, int64_t n, int64_t 
                              const double* src_y, int coord_mode, const float* tile_x0,
                              const float* tile_y0, const int64_t* tile_win,
                              int64_t win_h, int64_t win_w, double x_res, double y_res,
-                             int interp, double fill, int32_t* err_flags, void* stream) {
+                             int interp, double fill, void* workspace,
+                             int64_t workspace_bytes, int32_t* err_flags, void* stream) {
   using namespace xrs;
   if (interp != XRS_INTERP_NEAREST && interp != XRS_INTERP_BILINEAR &&
       interp != XRS_INTERP_TRIANGULAR) {
@@ -235,8 +407,15 @@ extern "C" int xrs_reproject(const void* src, int src_dtype, int64_t n, int64_t 
   if (!src || !dst || !src_x || !src_y || !tile_x0 || !tile_y0 || !tile_win || !err_flags ||
       n < 1 || src_h < 1 || src_w < 1 || dst_h < 1 || dst_w < 1 || tile_h < 1 || tile_w < 1 ||
       win_h < 1 || win_w < 1 || row_begin < 0 || row_end > dst_h || row_begin > row_end ||
-      src_rows < 0 || src_sy < src_w || (coord_mode != 0 && coord_mode != 1)) {
+      src_rows < 0 || src_sy < src_w || src_w > INT32_MAX || src_rows > INT32_MAX ||
+      (coord_mode != 0 && coord_mode != 1)) {
     xrs_set_error("xrs_reproject: invalid argument");
+    return XRS_ERR_ARG;
+  }
+  const int64_t need = xrs_reproject_workspace_size(dst_h, dst_w, tile_h, tile_w, coord_mode);
+  if (workspace_bytes < need || (need > 0 && !workspace)) {
+    xrs_set_error("xrs_reproject: workspace of %lld bytes required, %lld given",
+                  (long long)need, (long long)workspace_bytes);
     return XRS_ERR_ARG;
   }
   if (row_begin == row_end) return XRS_OK;
@@ -248,22 +427,31 @@ extern "C" int xrs_reproject(const void* src, int src_dtype, int64_t n, int64_t 
     xrs_set_error("xrs_reproject: bilinear output dtype must be float32 or float64");
     return XRS_ERR_ARG;
   }
-  ReprojectArgs a;
-  a.src = src; a.n = n; a.src_h = src_h; a.src_w = src_w; a.src_row0 = src_row0;
-  a.src_rows = src_rows; a.src_sn = src_sn; a.src_sy = src_sy;
-  a.dst = dst; a.dst_h = dst_h; a.dst_w = dst_w; a.row_begin = row_begin; a.row_end = row_end;
-  a.dst_sn = dst_sn; a.dst_sy = dst_sy; a.tile_h = tile_h; a.tile_w = tile_w;
-  a.ntiles_x = (dst_w + tile_w - 1) / tile_w;
-  a.src_x = src_x; a.src_y = src_y; a.tile_x0 = tile_x0; a.tile_y0 = tile_y0;
-  a.tile_win = tile_win; a.win_h = win_h; a.win_w = win_w;
-  a.x_res = x_res; a.neg_y_res = -y_res; a.fill = fill; a.err_flags = err_flags;
+  GatherArgs a;
+  Geometry& g = a.g;
+  g.src_h = src_h; g.src_w = src_w; g.src_row0 = src_row0; g.src_rows = src_rows;
+  g.dst_h = dst_h; g.dst_w = dst_w; g.row_begin = row_begin; g.row_end = row_end;
+  g.tile_h = tile_h; g.tile_w = tile_w;
+  g.ntiles_x = (dst_w + tile_w - 1) / tile_w;
+  g.ntiles_y = (dst_h + tile_h - 1) / tile_h;
+  g.src_x = src_x; g.src_y = src_y; g.tile_x0 = tile_x0; g.tile_y0 = tile_y0;
+  g.tile_win = tile_win; g.win_h = win_h; g.win_w = win_w;
+  g.x_res = x_res; g.neg_y_res = -y_res; g.err_flags = err_flags;
+  a.src = src; a.n = n; a.src_sn = src_sn; a.src_sy = src_sy;
+  a.dst = dst; a.dst_sn = dst_sn; a.dst_sy = dst_sy; a.fill = fill;
+  a.xtab = a.ytab = nullptr;
+  AxisEntry* xtab = static_cast<AxisEntry*>(workspace);
+  AxisEntry* ytab = xtab ? xtab + g.ntiles_x * g.ntiles_y * tile_w : nullptr;
   hipStream_t st = static_cast<hipStream_t>(stream);
 
   return dispatch_dtype(src_dtype, [&](auto tag) -> int {
     using T = decltype(tag);
-    if (interp == XRS_INTERP_NEAREST) return launch_coord<T, T, XRS_INTERP_NEAREST>(a, coord_mode, st);
-    if (interp == XRS_INTERP_TRIANGULAR) return launch_coord<T, T, XRS_INTERP_TRIANGULAR>(a, coord_mode, st);
-    if (dst_dtype == XRS_DTYPE_F32) return launch_coord<T, float, XRS_INTERP_BILINEAR>(a, coord_mode, st);
-    return launch_coord<T, double, XRS_INTERP_BILINEAR>(a, coord_mode, st);
+    if (interp == XRS_INTERP_NEAREST)
+      return launch<T, T, XRS_INTERP_NEAREST>(a, coord_mode, xtab, ytab, st);
+    if (interp == XRS_INTERP_TRIANGULAR)
+      return launch<T, T, XRS_INTERP_TRIANGULAR>(a, coord_mode, xtab, ytab, st);
+    if (dst_dtype == XRS_DTYPE_F32)
+      return launch<T, float, XRS_INTERP_BILINEAR>(a, coord_mode, xtab, ytab, st);
+    return launch<T, double, XRS_INTERP_BILINEAR>(a, coord_mode, xtab, ytab, st);
   });
 }

@@ -64,6 +64,10 @@ def reproject(src, plan, interp: str, fill: float, out_dtype=None, rows=None, ou
     if out is None:
         out = empty((n, r1 - r0, plan.dst_width), out_dtype, device)
     tables = plan.device_tables(device)
+    lib = _native.lib()
+    ws_bytes = lib.xrs_reproject_workspace_size(plan.dst_height, plan.dst_width, plan.tile_height,
+                                                plan.tile_width, plan.coord_mode)
+    ws = plan.workspace(device, ws_bytes)
     own_flags = flags is None
     if own_flags:
         flags = ErrorFlags(device)
@@ -71,14 +75,15 @@ def reproject(src, plan, interp: str, fill: float, out_dtype=None, rows=None, ou
     dn, dy, dx = out.stride()
     if sx != 1 or dx != 1:
         raise ValueError("innermost dimension must be contiguous")
-    rc = _native.lib().xrs_reproject(
+    rc = lib.xrs_reproject(
         ptr(src), src_dtype, n, plan.src_height, plan.src_width, src_row0, h_band, sn, sy,
         ptr(out), _native.dtype_code(out_dtype), plan.dst_height, plan.dst_width, r0, r1,
         dn, dy, plan.tile_height, plan.tile_width,
         ptr(tables["src_x"]), ptr(tables["src_y"]), plan.coord_mode,
         ptr(tables["tile_x0"]), ptr(tables["tile_y0"]), ptr(tables["tile_win"]),
         plan.win_height, plan.win_width, float(plan.x_res), float(plan.y_res),
-        interp_code, float(fill), flags.ptr, stream_handle(device, stream))
+        interp_code, float(fill), ptr(ws) if ws is not None else None, ws_bytes, flags.ptr,
+        stream_handle(device, stream))
     _native.check(rc, "xrs_reproject")
     if own_flags and check:
         flags.raise_if_set("reproject")

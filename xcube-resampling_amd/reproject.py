@@ -84,6 +84,17 @@ class ReprojectPlan:
             self._device_cache[key] = tabs
         return tabs
 
+    def workspace(self, device, nbytes: int):
+        """Device scratch for the axis tables (reused across calls; stream-ordered)."""
+        if nbytes <= 0:
+            return None
+        key = ("ws", str(device))
+        ws = self._device_cache.get(key)
+        if ws is None or ws.numel() < nbytes:
+            ws = torch().empty(nbytes, dtype=torch().uint8, device=device)
+            self._device_cache[key] = ws
+        return ws
+
     def source_rows_for(self, r0: int, r1: int) -> tuple[int, int]:
         """Global source rows [j0, j1) read by target rows [r0, r1) (clipped)."""
         tys = range(r0 // self.tile_height, (max(r1, r0 + 1) - 1) // self.tile_height + 1)
