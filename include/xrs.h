@@ -110,6 +110,55 @@ int xrs_reproject(const void* src, int src_dtype, int64_t n, int64_t src_h,
                   int interp, double fill, void* workspace,
                   int64_t workspace_bytes, int32_t* err_flags, void* stream);
 
+/* ---- aggregation codes (constants.py:51-65, coarsen.py) ------------------ */
+#define XRS_AGG_NONE 0
+#define XRS_AGG_MEAN 1
+#define XRS_AGG_SUM 2
+#define XRS_AGG_MAX 3
+#define XRS_AGG_MIN 4
+#define XRS_AGG_PROD 5
+#define XRS_AGG_COUNT 6
+#define XRS_AGG_FIRST 7
+#define XRS_AGG_LAST 8
+#define XRS_AGG_CENTER 9
+
+/* -------------------------------------------------------------------------
+ * xrs_affine — replaces affine._upscale (affine.py:316-362), i.e.
+ * dask_image.ndinterp.affine_transform -> scipy.ndimage.affine_transform
+ * (diagonal matrix, order 0/1, mode "constant", cval) evaluated per dask-image
+ * output chunk, and — with div_y/div_x > 1 — affine._downscale
+ * (affine.py:277-313): the div-x upscale fused with da.coarsen(agg).
+ *
+ * src: (nt, src_h, src_w) strides (src_st, src_sy, 1); dst: (nt, out_h,
+ *   out_w) strides (dst_st, dst_sy, 1) with dst_dtype = the reducer's numpy
+ *   result dtype (agg NONE: the scipy output dtype = src dtype, or float64
+ *   with recover_nan).
+ * Per axis (y, x) of the div-x intermediate (out_h*div_y, out_w*div_x):
+ *   scale, chunk = dask-image output chunk size, and per chunk k (device
+ *   arrays): rel[k] = first input index of the chunk's input slice, len[k] =
+ *   slice length, off[k] = offset + scale*chunk_offset - rel[k] (float64).
+ * t_next (device, nt entries, or NULL for 2-D data): index of the time slice
+ *   scipy multiplies by a zero weight (order 1), mirrored inside the time
+ *   chunk's input slice; -1 = none.
+ * recover_nan: affine.py:344-360 (NaN -> 0 image / (1 - mask) image ratio;
+ *   the host decides it with xrs_any_nan as the reference does with da.any).
+ * workspace: xrs_affine_workspace_size(out_h*div_y, out_w*div_x) bytes.
+ * ------------------------------------------------------------------------- */
+int64_t xrs_affine_workspace_size(int64_t inter_h, int64_t inter_w);
+
+int xrs_affine(const void* src, int src_dtype, int64_t nt, int64_t src_h, int64_t src_w,
+               int64_t src_st, int64_t src_sy, void* dst, int dst_dtype, int64_t out_h,
+               int64_t out_w, int64_t dst_st, int64_t dst_sy, int64_t div_y, int64_t div_x,
+               int agg, int order, double scale_y, double scale_x, int64_t chunk_y,
+               const int64_t* rel_y, const int64_t* len_y, const double* off_y,
+               int64_t chunk_x, const int64_t* rel_x, const int64_t* len_x,
+               const double* off_x, const int64_t* t_next, double cval, int recover_nan,
+               void* workspace, int64_t workspace_bytes, void* stream);
+
+/* *flag = 1 if any of the n elements of a float32/float64 device array is NaN
+ * (da.any(da.isnan(array)), affine.py:347-349); integer dtypes -> 0. */
+int xrs_any_nan(const void* src, int src_dtype, int64_t n, int32_t* flag, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,141 @@
+"""GPU parity tests of K2/K3 (xrs_affine): the reference's affine path
+(dask-image -> scipy order 0/1 + coarsen reducers).
+
+Bar: the reference's own test goldens (tests/test_affine.py, decimal 7 as
+there) through the Dataset API, and bit-exact equality with the oracle
+(dask-image restatement calling scipy itself + numpy reducers) on seeded
+random inputs covering upscale/downscale, 2-D/3-D, NaN/Inf, chunk edges,
+integer dtypes, every implemented reducer and recover_nans."""
+
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from fixtures import dataset_2x8x6_regular, dataset_8x6_regular, reference_goldens
+from helpers import assert_bitwise_equal
+from test_affine_cpu import CASES, RES
+
+pytestmark = pytest.mark.gpu
+GOLD = reference_goldens("tests/test_affine.py")
+
+
+@pytest.mark.parametrize("name,idx,size,xy_min,res,recover", CASES)
+def test_affine_transform_dataset_reference_goldens(name, idx, size, xy_min, res, recover):
+    import xcube_resampling_amd as xrs
+
+    ds = dataset_8x6_regular()
+    tgm = xrs.GridMapping.regular(size, xy_min, res, "EPSG:4326")
+    out = xrs.affine_transform_dataset(ds, tgm, interp_methods=1, recover_nans=recover)
+    exp, dec = GOLD[name][idx]
+    np.testing.assert_almost_equal(out["refl"].values, exp, decimal=dec)
+    assert set(out.variables) == set(ds.variables) | {"spatial_ref"}
+    assert out["refl"].shape == (size[1], size[0])
+
+
+def test_affine_3d_and_interp_forms():
+    import xcube_resampling_amd as xrs
+
+    ds3 = dataset_2x8x6_regular()
+    tgm = xrs.GridMapping.regular((3, 3), (50.0, 10.0), RES, "EPSG:4326")
+    out = xrs.affine_transform_dataset(ds3, tgm, interp_methods=1)
+    exp, dec = GOLD["test_subset_3d"][0]
+    np.testing.assert_almost_equal(out["refl"].values, exp, decimal=dec)
+    ds = dataset_8x6_regular()
+    for im in ("bilinear", {"refl": "bilinear"}, {"refl": 1}):
+        o = xrs.affine_transform_dataset(ds, tgm, source_gm=xrs.GridMapping.from_dataset(ds),
+                                         interp_methods=im)
+        np.testing.assert_almost_equal(o["refl"].values, GOLD["test_subset_with_source_gm"][0][0])
+
+
+def test_affine_errors():
+    import xcube_resampling_amd as xrs
+
+    ds = dataset_8x6_regular()
+    sgm = xrs.GridMapping.from_dataset(ds)
+    tgm = xrs.GridMapping.regular((8, 6), (50.2, 10.1), RES, sgm.crs)
+    with pytest.raises(ValueError, match="Higher order is not supported"):
+        xrs.affine_transform_dataset(ds, tgm, source_gm=sgm, interp_methods=3)
+    tgm = xrs.GridMapping.regular((3, 3), (50.05, 10.05), RES, "EPSG:3857")
+    with pytest.raises(AssertionError, match="Affine transformation cannot be applied"):
+        xrs.affine_transform_dataset(ds, tgm, source_gm=sgm)
+
+
+def _random_case(rng, dtype, nd, nan_frac):
+    shp = (int(rng.integers(1, 4)),) if nd == 3 else ()
+    shp += (int(rng.integers(20, 90)), int(rng.integers(20, 90)))
+    if np.issubdtype(dtype, np.floating):
+        a = (rng.random(shp) * 10 - 5).astype(dtype)
+        a.ravel()[rng.random(a.size) < nan_frac] = np.nan
+        if nan_frac:
+            a.ravel()[rng.integers(0, a.size)] = np.inf
+    else:
+        a = rng.integers(0, 200, shp).astype(dtype)
+    return a
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_kernel_matches_oracle_random(seed):
+    """Random affine matrices (up/down-scale, shifts), chunkings, dtypes and
+    reducers: engine == oracle bit for bit."""
+    import xcube_resampling_amd.affine as A
+    from oracle import affine_ref
+
+    rng = np.random.default_rng(1000 + seed)
+    dtype = [np.float32, np.float64, np.uint8, np.int16][seed % 4]
+    nd = 3 if seed % 3 == 0 else 2
+    a = _random_case(rng, dtype, nd, 0.02 if seed % 2 else 0.0)
+    h, w = a.shape[-2:]
+    interp = int(seed % 5 != 0)
+    s_i = float(rng.choice([0.5, 0.75, 1.0, 1.5, 2.0, 2.5, 4.0, 1 / 3]))
+    s_j = float(rng.choice([0.5, 0.9216, 1.0, 2.0, 3.0, 4.0]))
+    o_i, o_j = float(rng.uniform(-3, 3)), float(rng.choice([0.0, 0.5, -1.25, 2.0]))
+    matrix = ((s_i, 0.0, o_i), (0.0, s_j, o_j))
+    out_h, out_w = int(rng.integers(5, 40)), int(rng.integers(5, 40))
+    tile = (int(rng.integers(2, 20)), int(rng.integers(2, 20)))
+    lead = a.shape[:-2]
+    agg = ["mean", "sum", "max", "min", "count", "first", "last", "center", "prod"][seed % 9]
+    recover = bool(seed % 6 == 1)
+    fill = np.nan if np.issubdtype(dtype, np.floating) else 7
+    oshape = lead + (out_h, out_w)
+    ochunks = tuple(int(rng.integers(1, 3)) for _ in lead) + tile
+    ref = affine_ref.resample_array(a, matrix, oshape, ochunks, interp, agg, recover, fill)
+    got = A._resample_array(a, None, None, matrix, oshape, ochunks, interp, agg, recover, fill)
+    got = got if isinstance(got, np.ndarray) else got.cpu().numpy()
+    assert_bitwise_equal(got, np.asarray(ref), f"seed {seed} {dtype} {agg} interp={interp}")
+
+
+@pytest.mark.parametrize("agg", ["mean", "sum", "max", "min", "count", "first", "last",
+                                 "center", "prod"])
+def test_coarsen_4x4_matches_oracle(agg):
+    """Config-3 shape in miniature: 1024^2 f32 (0.1 % NaN) -> 256^2, scale 4."""
+    import xcube_resampling_amd.affine as A
+    from oracle import affine_ref
+
+    rng = np.random.default_rng(5)
+    a = rng.random((1024, 1024), dtype=np.float32)
+    a.ravel()[rng.choice(a.size, a.size // 1000, replace=False)] = np.nan
+    m = ((4.0, 0.0, 0.0), (0.0, 4.0, 0.0))
+    ref = affine_ref.resample_array(a, m, (256, 256), (128, 128), 1, agg, False, np.nan)
+    got = A._resample_array(a, None, None, m, (256, 256), (128, 128), 1, agg, False, np.nan)
+    assert_bitwise_equal(got.cpu().numpy(), np.asarray(ref), agg)
+
+
+def test_coarsen_via_dataset_api():
+    import xcube_resampling_amd as xrs
+    from oracle import affine_ref
+
+    rng = np.random.default_rng(9)
+    n = 512
+    a = rng.random((n, n), dtype=np.float32)
+    res = 2.0 ** -10
+    ds = xrs.Dataset(data_vars={"v": (("lat", "lon"), a)},
+                     coords={"lon": ("lon", (np.arange(n) + 0.5) * res),
+                             "lat": ("lat", 0.5 - (np.arange(n) + 0.5) * res)})
+    tgm = xrs.GridMapping.regular((n // 4, n // 4), (0, 0), 2.0 ** -8, "EPSG:4326", tile_size=64)
+    out = xrs.affine_transform_dataset(ds, tgm)  # float default: bilinear + mean
+    sgm = xrs.GridMapping.from_dataset(ds)
+    m = tgm.ij_transform_to(sgm)
+    assert m == ((4.0, 0.0, 0.0), (0.0, 4.0, 0.0))
+    ref = affine_ref.resample_array(a, m, (n // 4, n // 4), (64, 64), 1, "mean", False, np.nan)
+    assert_bitwise_equal(out["v"].values, ref)

@@ -12,6 +12,7 @@ from .crs import CRS, CRS_CRS84, CRS_WEBMERC, CRS_WGS84, Transformer
 from .dataset import DataArray, Dataset
 from .gridmapping import GridMapping
 from .options import get_options, set_options
+from .affine import affine_transform_dataset, resample_dataset
 from .reproject import plan_reproject, reproject_dataset
 
 __all__ = [
@@ -20,6 +21,8 @@ __all__ = [
     "CRS_WEBMERC",
     "CRS_WGS84",
     "DataArray",
+    "affine_transform_dataset",
+    "resample_dataset",
     "Dataset",
     "GridMapping",
     "LOG",

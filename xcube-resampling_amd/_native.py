@@ -68,7 +68,20 @@ _SIGNATURES = {
         _c_ptr, _c_i64, _c_ptr, _c_ptr,                                          # ws, flags, stream
     ]),
     "xrs_reproject_workspace_size": (_c_i64, [_c_i64, _c_i64, _c_i64, _c_i64, _c_int]),
+    "xrs_affine_workspace_size": (_c_i64, [_c_i64, _c_i64]),
+    "xrs_affine": (_c_int, [
+        _c_ptr, _c_int, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64,                  # src
+        _c_ptr, _c_int, _c_i64, _c_i64, _c_i64, _c_i64,                          # dst
+        _c_i64, _c_i64, _c_int, _c_int, _c_dbl, _c_dbl,                          # div, agg, order, scale
+        _c_i64, _c_ptr, _c_ptr, _c_ptr,                                          # y chunks
+        _c_i64, _c_ptr, _c_ptr, _c_ptr,                                          # x chunks
+        _c_ptr, _c_dbl, _c_int, _c_ptr, _c_i64, _c_ptr,                          # t_next .. stream
+    ]),
+    "xrs_any_nan": (_c_int, [_c_ptr, _c_int, _c_i64, _c_ptr, _c_ptr]),
 }
+
+AGG_CODES = {"mean": 1, "sum": 2, "max": 3, "min": 4, "prod": 5, "count": 6, "first": 7,
+             "last": 8, "center": 9}
 
 _lib = None
 _lock = threading.Lock()

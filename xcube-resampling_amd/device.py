@@ -77,6 +77,8 @@ def to_device(x, device, dtype=None):
 
 
 def empty(shape, dtype, device):
+    if np.dtype(dtype) == np.uint64:  # no torch uint64 arithmetic needed: bits only
+        return torch().empty(tuple(shape), dtype=torch().int64, device=device)
     return torch().empty(tuple(shape), dtype=torch_dtype(dtype), device=device)
 
 

@@ -97,3 +97,59 @@ def _np_dtype(t) -> np.dtype:
 
 def ij_bboxes(x_image, y_image, xy_bboxes, xy_border, ij_border):  # K4 (rectify path)
     raise NotImplementedError("ij_bboxes kernel not built yet")
+
+
+_WORKSPACES: dict = {}
+
+
+def _workspace(device, nbytes: int):
+    key = str(device)
+    ws = _WORKSPACES.get(key)
+    if ws is None or ws.numel() < nbytes:
+        ws = torch().empty(max(nbytes, 1), dtype=torch().uint8, device=device)
+        _WORKSPACES[key] = ws
+    return ws
+
+
+def any_nan(src, stream=None) -> bool:
+    """da.any(da.isnan(array)) on the device (affine.py:347-349)."""
+    device = src.device
+    flag = torch().zeros(1, dtype=torch().int32, device=device)
+    rc = _native.lib().xrs_any_nan(ptr(src), _native.DTYPE_CODES[_np_dtype(src)], src.numel(),
+                                   ptr(flag), stream_handle(device, stream))
+    _native.check(rc, "xrs_any_nan")
+    return bool(flag.item())
+
+
+def affine(src, plan, out=None, stream=None):
+    """K2/K3 — scipy order-0/1 affine resampling per dask-image chunk, fused
+    with the coarsen reducer when ``plan.div`` > 1.
+
+    src: device tensor (nt, H, W); plan: affine.AffinePlan.
+    Returns the device tensor (nt, out_h, out_w) in ``plan.out_dtype``.
+    """
+    device = src.device
+    nt, h, w = src.shape
+    if out is None:
+        out = empty((nt, plan.out_h, plan.out_w), plan.out_dtype, device)
+    tabs = plan.device_tables(device)
+    lib = _native.lib()
+    ih, iw = plan.out_h * plan.div_y, plan.out_w * plan.div_x
+    nbytes = lib.xrs_affine_workspace_size(ih, iw)
+    ws = _workspace(device, nbytes)
+    st, sy, sx = src.stride()
+    dt, dy, dx = out.stride()
+    if sx != 1 or dx != 1:
+        raise ValueError("innermost dimension must be contiguous")
+    out_code = _native.dtype_code(np.int64 if np.dtype(plan.out_dtype) == np.uint64
+                                  else plan.out_dtype)
+    rc = lib.xrs_affine(
+        ptr(src), _native.DTYPE_CODES[_np_dtype(src)], nt, h, w, st, sy,
+        ptr(out), out_code, plan.out_h, plan.out_w, dt, dy, plan.div_y, plan.div_x,
+        plan.agg_code, plan.order, float(plan.scale_y), float(plan.scale_x),
+        plan.chunk_y, ptr(tabs["rel_y"]), ptr(tabs["len_y"]), ptr(tabs["off_y"]),
+        plan.chunk_x, ptr(tabs["rel_x"]), ptr(tabs["len_x"]), ptr(tabs["off_x"]),
+        ptr(tabs["t_next"]) if tabs["t_next"] is not None else None,
+        float(plan.cval), int(plan.recover_nan), ptr(ws), nbytes, stream_handle(device, stream))
+    _native.check(rc, "xrs_affine")
+    return out
