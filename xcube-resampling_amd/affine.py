@@ -223,7 +223,7 @@ def plan_affine(src_shape, dtype, affine_matrix, output_shape, output_chunks, in
 def _resample_array(data, dims, chunks, affine_matrix, output_shape, output_chunks, interp,
                     agg, recover_nan, fill_value):
     """Device execution of affine.py:243-362 for one variable."""
-    if len(dims) > 3:
+    if len(data.shape) > 3:
         raise NotImplementedError("the engine resamples 2-D and 3-D variables")
     device = require_device()
     src = to_device(data, device)
