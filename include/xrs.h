@@ -159,6 +159,57 @@ int xrs_affine(const void* src, int src_dtype, int64_t nt, int64_t src_h, int64_
  * (da.any(da.isnan(array)), affine.py:347-349); integer dtypes -> 0. */
 int xrs_any_nan(const void* src, int src_dtype, int64_t n, int32_t* flag, void* stream);
 
+/* -------------------------------------------------------------------------
+ * xrs_ij_bboxes — replaces compute_ij_bboxes (gridmapping/bboxes.py:28-106;
+ * caller GridMapping.ij_bboxes_from_xy_bboxes, base.py:565-629): for every box
+ * the min/max source pixel (i, j) whose (x, y) lies inside the box (borders
+ * already applied by the caller: [x_min-b, x_max+b] etc., inclusive).
+ * x, y: (h, w) float64 device images, row stride sy.
+ * Grid mode (ntx > 0, ntx*nty == nboxes, box k = ty*ntx + tx): bx = (ntx, 2)
+ *   [x_min, x_max] per tile column, by = (nty, 2) [y_min, y_max] per tile row.
+ * Otherwise (ntx == 0): bx = (nboxes, 4) [x_min, y_min, x_max, y_max].
+ * acc: (nboxes, 4) int32 device accumulators, initialised by the caller to
+ *   {INT32_MAX, INT32_MAX, -1, -1}; receives {min i, min j, max i, max j}
+ *   (max i == -1: no pixel).  The ij_border expansion is host-side.
+ * ------------------------------------------------------------------------- */
+int xrs_ij_bboxes(const double* x, const double* y, int64_t h, int64_t w, int64_t sy,
+                  int64_t nboxes, int64_t ntx, int64_t nty, const double* bx,
+                  const double* by, int32_t* acc, void* stream);
+
+/* -------------------------------------------------------------------------
+ * xrs_rectify_ij — replaces _compute_target_source_ij_block and the numba
+ * kernels _compute_target_source_ij_sequential/_line (rectify.py:373-576):
+ * for every target pixel the fractional source pixel (i, j) of the FIRST
+ * source quad (raster order within the target tile's source bbox) whose
+ * triangle A or B contains the target pixel centre (tolerance uv_delta).
+ * x, y: (h, w) float64 source coordinates in the target CRS (row stride sy).
+ * tiles: device array of ntiles records {int32 r0, c0, th, tw, si0, sj0,
+ *   swin, shin; float64 x_off, y_off} (row-major, ntiles_x per row): target
+ *   tile origin/size, source window origin (si0 = -1: no source) and size,
+ *   and the reference's per-tile dst_x/y_offset.
+ * chunk_tile / chunk_q0 (device, nchunks): work list of 256-quad chunks.
+ * x_scale = dst_x_res; y_scale = dst_y_res (j-axis up) or -dst_y_res.
+ * keys: (dst_h, dst_w) uint32 scratch; ij: (2, dst_h, dst_w) float64 output
+ *   (NaN where no quad hits).
+ * ------------------------------------------------------------------------- */
+int xrs_rectify_ij(const double* x, const double* y, int64_t h, int64_t w, int64_t sy,
+                   const void* tiles, int64_t ntiles, int64_t ntiles_x,
+                   const int64_t* chunk_tile, const int64_t* chunk_q0, int64_t nchunks,
+                   int64_t dst_h, int64_t dst_w, double x_scale, double y_scale,
+                   double uv_delta, uint32_t* keys, double* ij, void* stream);
+
+/* -------------------------------------------------------------------------
+ * xrs_rectify_var — replaces _compute_var_image_block / _sequential /
+ * _for_dest_line (rectify.py:605-734): sample a (n, src_h, src_w) variable
+ * at the fractional source positions ij (2, dst_h, dst_w); nearest (u > 0.5
+ * rounds up), triangular or bilinear in float64, stored in the variable
+ * dtype; NaN positions -> fill.  dst: (n, dst_h, dst_w), slice stride dst_sn.
+ * ------------------------------------------------------------------------- */
+int xrs_rectify_var(const double* ij, int64_t dst_h, int64_t dst_w, const void* src,
+                    int src_dtype, int64_t n, int64_t src_h, int64_t src_w, int64_t src_sn,
+                    int64_t src_sy, void* dst, int64_t dst_sn, int interp, double fill,
+                    void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -99,6 +99,91 @@ def reproject_case(name, data, src_lon, src_lat, x_res, y_res, tsize, txy_min, t
           f"windows {wx}x{wy}, pad {pad}")
 
 
+class _ValuesView:
+    """Stand-in for an xarray.DataArray inside the reference block functions
+    (only slicing + .values are used)."""
+
+    def __init__(self, a):
+        self._a = np.asarray(a)
+
+    def __getitem__(self, k):
+        return _ValuesView(self._a[k])
+
+    @property
+    def values(self):
+        return self._a
+
+    @property
+    def shape(self):
+        return self._a.shape
+
+    @property
+    def dtype(self):
+        return self._a.dtype
+
+
+def _swath(rng, h, w, lon0, lat0, dlon_i, dlon_j, dlat_i, dlat_j, curv, jitter):
+    i = np.arange(w)[None, :]
+    j = np.arange(h)[:, None]
+    lon = lon0 + dlon_i * i + dlon_j * j
+    lat = lat0 - dlat_j * j - dlat_i * i + curv * (i - w / 2) ** 2
+    lon = lon + rng.normal(0, jitter * dlon_i, (h, w))
+    lat = lat + rng.normal(0, jitter * dlat_j, (h, w))
+    return lon, lat
+
+
+def rectify_case(name, rng, h, w, size, xy_min, res, tile, nvar, dtype, j_up=False, nan_px=0):
+    ref = load_functions("xcube_resampling/rectify.py", [
+        "_compute_target_source_ij_block", "_compute_target_source_ij_sequential",
+        "_compute_target_source_ij_line", "_compute_var_image_block",
+        "_compute_var_image_sequential", "_compute_var_image_for_dest_line",
+        "_fdet", "_fu", "_fv", "_fclamp", "_iclamp"])
+    bb = load_functions("xcube_resampling/gridmapping/bboxes.py", ["compute_ij_bboxes"])
+    lon, lat = _swath(rng, h, w, 5.0, 60.0, 0.045, 0.009, 0.004, 0.027, 1e-6, 0.05)
+    if nan_px:
+        lon.ravel()[rng.choice(lon.size, nan_px, replace=False)] = np.nan
+    if np.issubdtype(dtype, np.floating):
+        var = rng.random((nvar, h, w)).astype(dtype)
+    else:
+        var = rng.integers(0, 250, (nvar, h, w)).astype(dtype)
+    W, H = size
+    tw, th = tile
+    geo = gref.regular_geometry(size, xy_min, res, tile_size=tile, is_j_axis_up=j_up)
+    x_min, y_min, x_max, y_max = geo["xy_bbox"]
+    x_res, y_res = geo["xy_res"]
+    xy_border = min(min(2 * (W / tw) * x_res, 2 * (H / th) * y_res),
+                    min(0.5 * (x_max - x_min), 0.5 * (y_max - y_min)))
+    boxes = geo["xy_bboxes"]
+    ij_bboxes = np.full_like(boxes, -1, dtype=np.int64)
+    bb["compute_ij_bboxes"](lon, lat, boxes, xy_border, 1, ij_bboxes)
+    xy = _ValuesView(np.stack([lon, lat]))
+    ij = np.full((2, H, W), np.nan)
+    k = 0
+    tiles = [(r0, min(H, r0 + th), c0, min(W, c0 + tw)) for r0 in range(0, H, th)
+             for c0 in range(0, W, tw)]
+    for (r0, r1, c0, c1) in tiles:
+        blk = ref["_compute_target_source_ij_block"](
+            np.float64, k, (2, r1 - r0, c1 - c0), ((0, 2), (r0, r1), (c0, c1)), xy, ij_bboxes,
+            x_min, y_min, y_max, x_res, y_res, j_up, 1e-3)
+        ij[:, r0:r1, c0:c1] = blk
+        k += 1
+    outs = {}
+    fill = np.nan if np.issubdtype(dtype, np.floating) else 255
+    for interp in ("nearest", "bilinear", "triangular"):
+        res_ = np.empty((nvar, H, W), dtype=dtype)
+        for (r0, r1, c0, c1) in tiles:
+            blk = ref["_compute_var_image_block"](ij[:, r0:r1, c0:c1], _ValuesView(var), fill,
+                                                  interp, (nvar, r1 - r0, c1 - c0))
+            res_[:, r0:r1, c0:c1] = blk
+        outs[f"out_{interp}"] = res_
+    np.savez_compressed(os.path.join(HERE, f"rectify_{name}.npz"), lon=lon, lat=lat, var=var,
+                        size=np.array(size), xy_min=np.array(xy_min, float),
+                        res=np.array(res, float), tile=np.array(tile), j_up=j_up, fill=fill,
+                        xy_border=xy_border, ij_bboxes=ij_bboxes, ij=ij, **outs)
+    print(f"rectify_{name}: src {h}x{w} -> {size} tiles {tile}, "
+          f"{int(np.sum(~np.isnan(ij[0])))} px with a source")
+
+
 def main():
     rng = np.random.default_rng(SEED)
     # 1) float32 (n=2), lon/lat 4326 source, 3857 target with partial edge tiles
@@ -122,6 +207,13 @@ def main():
     d = rng.random((1, h, w), dtype=np.float32)
     reproject_case("pad", d, lon, lat, x_res, y_res, (50, 40), (-1400000.0, 5600000.0),
                    (25000, 40000), (25, 20), ["nearest", "bilinear", "triangular"], np.nan)
+    # rectify: OLCI-like jittered swath, tiled target, finer/coarser targets
+    rectify_case("f32", rng, 24, 30, (40, 30), (5.0, 59.1), 0.03, (16, 12), 2, np.float32)
+    rectify_case("fine", rng, 12, 14, (50, 44), (5.05, 59.5), 0.012, (20, 20), 1, np.float64)
+    rectify_case("u8_jup", rng, 20, 22, (30, 26), (5.0, 59.3), 0.03, (11, 9), 1, np.uint8,
+                 j_up=True)
+    rectify_case("nan", rng, 22, 26, (36, 28), (5.0, 59.2), 0.03, (13, 15), 1, np.float32,
+                 nan_px=6)
 
 
 if __name__ == "__main__":

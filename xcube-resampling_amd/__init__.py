@@ -14,6 +14,8 @@ from .gridmapping import GridMapping
 from .options import get_options, set_options
 from .affine import affine_transform_dataset, resample_dataset
 from .reproject import plan_reproject, reproject_dataset
+from .rectify import rectify_dataset
+from .spatial import resample_in_space
 
 __all__ = [
     "CRS",
@@ -29,6 +31,8 @@ __all__ = [
     "Transformer",
     "get_options",
     "plan_reproject",
+    "rectify_dataset",
     "reproject_dataset",
+    "resample_in_space",
     "set_options",
 ]

@@ -78,6 +78,13 @@ _SIGNATURES = {
         _c_ptr, _c_dbl, _c_int, _c_ptr, _c_i64, _c_ptr,                          # t_next .. stream
     ]),
     "xrs_any_nan": (_c_int, [_c_ptr, _c_int, _c_i64, _c_ptr, _c_ptr]),
+    "xrs_ij_bboxes": (_c_int, [_c_ptr, _c_ptr, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64,
+                               _c_ptr, _c_ptr, _c_ptr, _c_ptr]),
+    "xrs_rectify_ij": (_c_int, [_c_ptr, _c_ptr, _c_i64, _c_i64, _c_i64, _c_ptr, _c_i64, _c_i64,
+                                _c_ptr, _c_ptr, _c_i64, _c_i64, _c_i64, _c_dbl, _c_dbl, _c_dbl,
+                                _c_ptr, _c_ptr, _c_ptr]),
+    "xrs_rectify_var": (_c_int, [_c_ptr, _c_i64, _c_i64, _c_ptr, _c_int, _c_i64, _c_i64, _c_i64,
+                                 _c_i64, _c_i64, _c_ptr, _c_i64, _c_int, _c_dbl, _c_ptr]),
 }
 
 AGG_CODES = {"mean": 1, "sum": 2, "max": 3, "min": 4, "prod": 5, "count": 6, "first": 7,

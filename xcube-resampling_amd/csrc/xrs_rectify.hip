@@ -1,0 +1,428 @@
+// xrs_rectify.hip — K4/K5/K6: irregular (2-D coordinates) -> regular grid for gfx950.
+//
+// K4 ij_bboxes   replaces gridmapping/bboxes.py:28-106 (compute_ij_bboxes, a
+//                numba prange over boxes scanning every source pixel).  Here
+//                every source pixel is visited once: each lane finds the boxes
+//                that contain its (x, y) (for a tile grid only the matching
+//                tile columns x rows), and the wave merges equal boxes with a
+//                ballot-driven loop (wave min of the next candidate box, DPP/
+//                shuffle min/max reductions, one lane issues the atomics) —
+//                4 atomics per (wave, box) instead of per pixel.
+// K5 rectify_ij  replaces rectify.py:373-576 (_compute_target_source_ij_block
+//                -> _sequential -> _line): for every target tile, the source
+//                quads inside its source bbox rasterise into the tile.  The
+//                reference keeps the FIRST quad in raster order that hits a
+//                target pixel; that is the minimum raster key of all hitting
+//                quads, so K5a claims pixels with atomicMin (order-independent)
+//                and K5b recomputes the winning quad's barycentric (u, v) with
+//                the identical float64 expressions (_fdet/_fu/_fv, 737-768).
+// K6 rectify_var replaces rectify.py:605-734 (_compute_var_image_block): per
+//                target pixel, source sub-pixel position -> nearest /
+//                triangular / bilinear in float64, stored in the variable dtype.
+//                Formulated on global indices; the reference's per-tile source
+//                sub-window (622-630) shifts indices by an integer, which leaves
+//                every index, fraction and clamp unchanged.
+
+#include <cmath>
+
+#include "xrs_common.hpp"
+
+namespace xrs {
+namespace {
+
+constexpr int kThreads = 256;
+
+// ---- wave-level helpers (64 lanes) ------------------------------------------
+__device__ inline int32_t wave_min(int32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ inline int32_t wave_max(int32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// ---- K4 ----------------------------------------------------------------------
+struct BBoxArgs {
+  const double* x;        // source x image (h, w), row stride sy
+  const double* y;
+  int64_t h, w, sy;
+  int64_t nboxes;
+  // grid mode (ntx*nty == nboxes): box k = ty*ntx + tx has x range of column
+  // tx and y range of row ty; otherwise every box is tested (ntx == 0)
+  int64_t ntx, nty;
+  const double* bx;       // grid: (ntx, 2) [x_min, x_max] (border included); else (nboxes, 4)
+  const double* by;       // grid: (nty, 2) [y_min, y_max]
+  int32_t* acc;           // (nboxes, 4): min i, min j, max i, max j
+};
+
+// Next candidate box > `after` that contains (x, y), or INT32_MAX.
+__device__ inline int32_t next_box(const BBoxArgs& a, double x, double y, int32_t tx0, int32_t tx1,
+                                   int32_t ty0, int32_t ty1, int32_t after) {
+  if (a.ntx > 0) {  // grid: candidates = rectangle [ty0,ty1] x [tx0,tx1], row-major
+    if (tx0 > tx1 || ty0 > ty1) return INT32_MAX;
+    int32_t ty = ty0, tx = tx0;
+    if (after >= 0) {
+      ty = after / (int32_t)a.ntx;
+      tx = after - ty * (int32_t)a.ntx + 1;
+      if (tx > tx1) { tx = tx0; ++ty; }
+      if (ty < ty0) { ty = ty0; tx = tx0; }
+    }
+    return ty <= ty1 ? ty * (int32_t)a.ntx + tx : INT32_MAX;
+  }
+  for (int32_t k = after + 1; k < (int32_t)a.nboxes; ++k) {
+    const double* b = a.bx + 4 * k;
+    if (b[0] <= x && x <= b[2] && b[1] <= y && y <= b[3]) return k;
+  }
+  return INT32_MAX;
+}
+
+__global__ void __launch_bounds__(kThreads)
+ij_bboxes_kernel(BBoxArgs a) {
+  const int64_t n = a.h * a.w;
+  const int64_t stride = (int64_t)gridDim.x * kThreads;
+  // every lane of a wave iterates the same number of times (wave-uniform trip
+  // count), so the wave-wide shuffles below always see all 64 lanes
+  for (int64_t base = (int64_t)blockIdx.x * kThreads; base < n; base += stride) {
+    const int64_t idx = base + threadIdx.x;
+    const bool valid = idx < n;
+    double x = NAN, y = NAN;
+    int32_t i0 = 0, j0 = 0;
+    if (valid) {
+      j0 = (int32_t)(idx / a.w);
+      i0 = (int32_t)(idx - (int64_t)j0 * a.w);
+      x = a.x[(int64_t)j0 * a.sy + i0];
+      y = a.y[(int64_t)j0 * a.sy + i0];
+    }
+    int32_t tx0 = 1, tx1 = 0, ty0 = 1, ty1 = 0;
+    if (valid && a.ntx > 0) {  // x_min <= x <= x_max, y_min <= y <= y_max (bboxes.py:60-69)
+      for (int32_t t = 0; t < (int32_t)a.ntx; ++t)
+        if (a.bx[2 * t] <= x && x <= a.bx[2 * t + 1]) { if (tx0 > tx1) tx0 = t; tx1 = t; }
+      for (int32_t t = 0; t < (int32_t)a.nty; ++t)
+        if (a.by[2 * t] <= y && y <= a.by[2 * t + 1]) { if (ty0 > ty1) ty0 = t; ty1 = t; }
+    }
+    int32_t cur = valid ? next_box(a, x, y, tx0, tx1, ty0, ty1, -1) : INT32_MAX;
+    while (true) {
+      const int32_t k = wave_min(cur);  // next box any lane of the wave contributes to
+      if (k == INT32_MAX) break;
+      const bool mine = cur == k;
+      const int32_t imin = wave_min(mine ? i0 : INT32_MAX);
+      const int32_t jmin = wave_min(mine ? j0 : INT32_MAX);
+      const int32_t imax = wave_max(mine ? i0 : -1);
+      const int32_t jmax = wave_max(mine ? j0 : -1);
+      if ((threadIdx.x & 63) == 0) {
+        atomicMin(&a.acc[4 * k + 0], imin);
+        atomicMin(&a.acc[4 * k + 1], jmin);
+        atomicMax(&a.acc[4 * k + 2], imax);
+        atomicMax(&a.acc[4 * k + 3], jmax);
+      }
+      if (mine) cur = next_box(a, x, y, tx0, tx1, ty0, ty1, k);
+    }
+  }
+}
+
+// ---- rectify geometry (rectify.py:737-773) -----------------------------------
+__device__ inline double fdet(double px0, double py0, double px1, double py1, double px2,
+                              double py2) {
+  return (px0 - px1) * (py0 - py2) - (px0 - px2) * (py0 - py1);
+}
+__device__ inline double fu(double px, double py, double px0, double py0, double px2,
+                            double py2) {
+  return (px0 - px) * (py0 - py2) - (py0 - py) * (px0 - px2);
+}
+__device__ inline double fv(double px, double py, double px0, double py0, double px1,
+                            double py1) {
+  return (py0 - py) * (px0 - px1) - (px0 - px) * (py0 - py1);
+}
+__device__ inline double fclamp(double x, double lo, double hi) {
+  return x < lo ? lo : (x > hi ? hi : x);
+}
+
+struct TileInfo {      // one target tile (host-computed, rectify.py:391-418)
+  int32_t r0, c0;      // first target row / column of the tile
+  int32_t th, tw;      // tile height / width (edge tiles are short)
+  int32_t si0, sj0;    // src_i_min, src_j_min (-1: no source)
+  int32_t swin, shin;  // source window width / height (i_max+1-i_min clipped)
+  double x_off, y_off; // dst_x_offset, dst_y_offset
+};
+
+struct RectArgs {
+  const double* x;     // source coordinates (h, w) in the target CRS
+  const double* y;
+  int64_t h, w, sy;
+  const TileInfo* tiles;
+  int64_t ntiles;
+  const int64_t* chunk_tile;   // work chunks: tile of chunk c
+  const int64_t* chunk_q0;     // first quad of chunk c (tile-local, raster order)
+  int64_t nchunks;
+  int64_t dst_h, dst_w;
+  double x_scale, y_scale;     // dst_x_res, dst_y_res (negated when j-axis down)
+  double uv_delta;
+  uint32_t* keys;              // (dst_h, dst_w) claim keys, 0xFFFFFFFF = free
+  double* ij;                  // (2, dst_h, dst_w) output
+};
+
+// Test triangle A then B of quad (qj, qi) (global source indices) for the
+// target pixel centre (dx, dy) (rectify.py:556-573).  Returns 0 (no hit), 1
+// (triangle A: src = p0 + clamp(u, v)) or 2 (triangle B: src = p3 - clamp(u, v));
+// cu, cv receive the clamped barycentric coordinates.
+__device__ inline int quad_hit(const RectArgs& a, int64_t qj, int64_t qi, double dx, double dy,
+                               double det_a, double det_b, double& cu, double& cv) {
+  const double* X = a.x;
+  const double* Y = a.y;
+  const int64_t r0 = qj * a.sy, r1 = (qj + 1) * a.sy;
+  const double p0x = X[r0 + qi], p1x = X[r0 + qi + 1], p2x = X[r1 + qi], p3x = X[r1 + qi + 1];
+  const double p0y = Y[r0 + qi], p1y = Y[r0 + qi + 1], p2y = Y[r1 + qi], p3y = Y[r1 + qi + 1];
+  const double umin = -a.uv_delta, vmin = -a.uv_delta, uvmax = 1.0 + 2 * a.uv_delta;
+  if (det_a != 0.0) {
+    const double u = fu(dx, dy, p0x, p0y, p2x, p2y) / det_a;
+    const double v = fv(dx, dy, p0x, p0y, p1x, p1y) / det_a;
+    if (u >= umin && v >= vmin && u + v <= uvmax) {
+      cu = fclamp(u, 0.0, 1.0);
+      cv = fclamp(v, 0.0, 1.0);
+      return 1;
+    }
+  }
+  if (det_b != 0.0) {
+    const double u = fu(dx, dy, p3x, p3y, p1x, p1y) / det_b;
+    const double v = fv(dx, dy, p3x, p3y, p2x, p2y) / det_b;
+    if (u >= umin && v >= vmin && u + v <= uvmax) {
+      cu = fclamp(u, 0.0, 1.0);
+      cv = fclamp(v, 0.0, 1.0);
+      return 2;
+    }
+  }
+  return 0;
+}
+
+__device__ inline void quad_dets(const RectArgs& a, int64_t qj, int64_t qi, double& det_a,
+                                 double& det_b) {
+  const int64_t r0 = qj * a.sy, r1 = (qj + 1) * a.sy;
+  const double p0x = a.x[r0 + qi], p1x = a.x[r0 + qi + 1], p2x = a.x[r1 + qi],
+               p3x = a.x[r1 + qi + 1];
+  const double p0y = a.y[r0 + qi], p1y = a.y[r0 + qi + 1], p2y = a.y[r1 + qi],
+               p3y = a.y[r1 + qi + 1];
+  det_a = fdet(p0x, p0y, p1x, p1y, p2x, p2y);
+  if (det_a != det_a) det_a = 0.0;
+  det_b = fdet(p3x, p3y, p2x, p2y, p1x, p1y);
+  if (det_b != det_b) det_b = 0.0;
+}
+
+// ---- K5a: claim target pixels with the raster-order key of hitting quads -------
+__global__ void __launch_bounds__(kThreads)
+rectify_claim_kernel(RectArgs a) {
+  for (int64_t c = blockIdx.x; c < a.nchunks; c += gridDim.x) {
+    const TileInfo ti = a.tiles[a.chunk_tile[c]];
+    const int64_t nq_i = ti.swin - 1;
+    const int64_t q = a.chunk_q0[c] + threadIdx.x;
+    if (ti.si0 < 0 || nq_i <= 0 || q >= nq_i * (int64_t)(ti.shin - 1)) continue;
+    const int64_t lj = q / nq_i, li = q - lj * nq_i;       // quad within the tile window
+    const int64_t qj = ti.sj0 + lj, qi = ti.si0 + li;       // global quad corner p0
+    const int64_t r0 = qj * a.sy, r1 = (qj + 1) * a.sy;
+    const double px[4] = {a.x[r0 + qi], a.x[r0 + qi + 1], a.x[r1 + qi], a.x[r1 + qi + 1]};
+    const double py[4] = {a.y[r0 + qi], a.y[r0 + qi + 1], a.y[r1 + qi], a.y[r1 + qi + 1]};
+    int64_t imin = INT64_MAX, imax = INT64_MIN, jmin = INT64_MAX, jmax = INT64_MIN;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {  // np.floor(...).astype(np.int64)  (rectify.py:500-501)
+      const int64_t pi = f64_to_i64_x86(floor((px[k] - ti.x_off) / a.x_scale));
+      const int64_t pj = f64_to_i64_x86(floor((py[k] - ti.y_off) / a.y_scale));
+      imin = min(imin, pi); imax = max(imax, pi);
+      jmin = min(jmin, pj); jmax = max(jmax, pj);
+    }
+    if (imax < 0 || jmax < 0 || imin >= ti.tw || jmin >= ti.th) continue;
+    imin = max(imin, (int64_t)0); jmin = max(jmin, (int64_t)0);
+    imax = min(imax, (int64_t)ti.tw - 1); jmax = min(jmax, (int64_t)ti.th - 1);
+    double det_a, det_b;
+    quad_dets(a, qj, qi, det_a, det_b);
+    if (det_a == 0.0 && det_b == 0.0) continue;
+    const uint32_t key = (uint32_t)(qj * a.w + qi);
+    for (int64_t dj = jmin; dj <= jmax; ++dj) {
+      const double dy = ti.y_off + ((double)dj + 0.5) * a.y_scale;
+      uint32_t* krow = a.keys + (int64_t)(ti.r0 + dj) * a.dst_w + ti.c0;
+      for (int64_t di = imin; di <= imax; ++di) {
+        if (krow[di] <= key) continue;  // already claimed by an earlier quad
+        const double dx = ti.x_off + ((double)di + 0.5) * a.x_scale;
+        double cu, cv;
+        if (quad_hit(a, qj, qi, dx, dy, det_a, det_b, cu, cv)) atomicMin(&krow[di], key);
+      }
+    }
+  }
+}
+
+// ---- K5b: resolve the winning quad of every target pixel ------------------------
+__global__ void __launch_bounds__(kThreads)
+rectify_resolve_kernel(RectArgs a, int64_t ntiles_x) {
+  const int64_t n = a.dst_h * a.dst_w;
+  for (int64_t p = (int64_t)blockIdx.x * kThreads + threadIdx.x; p < n;
+       p += (int64_t)gridDim.x * kThreads) {
+    const uint32_t key = a.keys[p];
+    double oi = NAN, oj = NAN;
+    if (key != 0xFFFFFFFFu) {
+      const int64_t r = p / a.dst_w, c = p - r * a.dst_w;
+      const TileInfo& ti0 = a.tiles[0];
+      const int64_t t = (r / ti0.th) * ntiles_x + c / ti0.tw;  // tile 0 has the full tile size
+      const TileInfo ti = a.tiles[t];
+      const int64_t qj = key / a.w, qi = key - qj * a.w;
+      double det_a, det_b;
+      quad_dets(a, qj, qi, det_a, det_b);
+      const int64_t dj = r - ti.r0, di = c - ti.c0;
+      const double dy = ti.y_off + ((double)dj + 0.5) * a.y_scale;
+      const double dx = ti.x_off + ((double)di + 0.5) * a.x_scale;
+      double cu, cv;
+      const int tri = quad_hit(a, qj, qi, dx, dy, det_a, det_b, cu, cv);
+      if (tri) {
+        const int64_t li = qi - ti.si0, lj = qj - ti.sj0;   // tile-local quad indices
+        double src_i, src_j;
+        if (tri == 1) {
+          src_i = (double)li + cu;                           // src_i0 + clamp(u)
+          src_j = (double)lj + cv;
+        } else {
+          src_i = (double)(li + 1) - cu;                     // src_i1 - clamp(u)
+          src_j = (double)(lj + 1) - cv;
+        }
+        oi = (double)ti.si0 + src_i;                         // src_i_min + src_i
+        oj = (double)ti.sj0 + src_j;
+      }
+    }
+    a.ij[p] = oi;
+    a.ij[n + p] = oj;
+  }
+}
+
+// ---- K6: per-variable sampling (rectify.py:663-734) ------------------------------
+template <typename T, int INTERP>
+__global__ void __launch_bounds__(kThreads)
+rectify_var_kernel(const double* __restrict__ ij, int64_t dst_h, int64_t dst_w,
+                   const T* __restrict__ src, int64_t n, int64_t src_h, int64_t src_w,
+                   int64_t src_sn, int64_t src_sy, T* __restrict__ dst, int64_t dst_sn,
+                   double fill) {
+  const int64_t np = dst_h * dst_w;
+  const T tfill = Conv<T>::from_f64(fill);
+  for (int64_t p = (int64_t)blockIdx.x * kThreads + threadIdx.x; p < np;
+       p += (int64_t)gridDim.x * kThreads) {
+    const double fi = ij[p], fj = ij[np + p];
+    if (fi != fi || fj != fj) {
+      for (int64_t s = 0; s < n; ++s) dst[s * dst_sn + p] = tfill;
+      continue;
+    }
+    int64_t i0 = (int64_t)fi, j0 = (int64_t)fj;   // int() truncation (values >= 0)
+    const double u = fi - (double)i0, v = fj - (double)j0;
+    const int64_t imax = src_w - 1, jmax = src_h - 1;
+    if (INTERP == XRS_INTERP_NEAREST) {
+      if (u > 0.5) i0 = min(max(i0 + 1, (int64_t)0), imax);
+      if (v > 0.5) j0 = min(max(j0 + 1, (int64_t)0), jmax);
+      for (int64_t s = 0; s < n; ++s) dst[s * dst_sn + p] = src[s * src_sn + j0 * src_sy + i0];
+      continue;
+    }
+    const int64_t i1 = min(max(i0 + 1, (int64_t)0), imax), j1 = min(max(j0 + 1, (int64_t)0), jmax);
+    for (int64_t s = 0; s < n; ++s) {
+      const T* S = src + s * src_sn;
+      double val;
+      const double v01 = (double)S[j0 * src_sy + i1], v10 = (double)S[j1 * src_sy + i0];
+      if (INTERP == XRS_INTERP_TRIANGULAR) {
+        if (u + v < 1.0) {
+          const double v00 = (double)S[j0 * src_sy + i0];
+          val = v00 + u * (v01 - v00) + v * (v10 - v00);
+        } else {
+          const double v11 = (double)S[j1 * src_sy + i1];
+          val = v11 + (1.0 - u) * (v10 - v11) + (1.0 - v) * (v01 - v11);
+        }
+      } else {
+        const double v00 = (double)S[j0 * src_sy + i0], v11 = (double)S[j1 * src_sy + i1];
+        const double u0 = v00 + u * (v01 - v00);
+        const double u1 = v10 + u * (v11 - v10);
+        val = u0 + v * (u1 - u0);
+      }
+      dst[s * dst_sn + p] = Conv<T>::from_f64(val);
+    }
+  }
+}
+
+}  // namespace
+}  // namespace xrs
+
+extern "C" int xrs_ij_bboxes(const double* x, const double* y, int64_t h, int64_t w,
+                             int64_t sy, int64_t nboxes, int64_t ntx, int64_t nty,
+                             const double* bx, const double* by, int32_t* acc, void* stream) {
+  using namespace xrs;
+  if (!x || !y || !bx || !acc || h < 1 || w < 1 || sy < w || nboxes < 0 ||
+      (ntx > 0 && (ntx * nty != nboxes || !by)) || h * w > INT32_MAX) {
+    xrs_set_error("xrs_ij_bboxes: invalid argument");
+    return XRS_ERR_ARG;
+  }
+  if (nboxes == 0) return XRS_OK;
+  BBoxArgs a{x, y, h, w, sy, nboxes, ntx, nty, bx, by, acc};
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const int nb = grid_blocks(h * w, kThreads, 256 * 8);
+  hipLaunchKernelGGL(ij_bboxes_kernel, dim3(nb), dim3(kThreads), 0, st, a);
+  XRS_HIP_CHECK(hipGetLastError());
+  return XRS_OK;
+}
+
+extern "C" int xrs_rectify_ij(const double* x, const double* y, int64_t h, int64_t w,
+                              int64_t sy, const void* tiles, int64_t ntiles, int64_t ntiles_x,
+                              const int64_t* chunk_tile, const int64_t* chunk_q0,
+                              int64_t nchunks, int64_t dst_h, int64_t dst_w, double x_scale,
+                              double y_scale, double uv_delta, uint32_t* keys, double* ij,
+                              void* stream) {
+  using namespace xrs;
+  if (!x || !y || !tiles || !keys || !ij || h < 2 || w < 2 || sy < w || ntiles < 1 ||
+      dst_h < 1 || dst_w < 1 || h * w >= (int64_t)UINT32_MAX || (nchunks > 0 && (!chunk_tile || !chunk_q0))) {
+    xrs_set_error("xrs_rectify_ij: invalid argument");
+    return XRS_ERR_ARG;
+  }
+  RectArgs a;
+  a.x = x; a.y = y; a.h = h; a.w = w; a.sy = sy;
+  a.tiles = static_cast<const TileInfo*>(tiles); a.ntiles = ntiles;
+  a.chunk_tile = chunk_tile; a.chunk_q0 = chunk_q0; a.nchunks = nchunks;
+  a.dst_h = dst_h; a.dst_w = dst_w; a.x_scale = x_scale; a.y_scale = y_scale;
+  a.uv_delta = uv_delta; a.keys = keys; a.ij = ij;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  XRS_HIP_CHECK(hipMemsetAsync(keys, 0xFF, (size_t)(dst_h * dst_w) * sizeof(uint32_t), st));
+  if (nchunks > 0) {
+    const int nb = grid_blocks(nchunks, 1, 256 * 8);
+    hipLaunchKernelGGL(rectify_claim_kernel, dim3(nb), dim3(kThreads), 0, st, a);
+    XRS_HIP_CHECK(hipGetLastError());
+  }
+  const int nb2 = grid_blocks(dst_h * dst_w, kThreads, 256 * 8);
+  hipLaunchKernelGGL(rectify_resolve_kernel, dim3(nb2), dim3(kThreads), 0, st, a, ntiles_x);
+  XRS_HIP_CHECK(hipGetLastError());
+  return XRS_OK;
+}
+
+extern "C" int xrs_rectify_var(const double* ij, int64_t dst_h, int64_t dst_w, const void* src,
+                               int src_dtype, int64_t n, int64_t src_h, int64_t src_w,
+                               int64_t src_sn, int64_t src_sy, void* dst, int64_t dst_sn,
+                               int interp, double fill, void* stream) {
+  using namespace xrs;
+  if (interp != XRS_INTERP_NEAREST && interp != XRS_INTERP_BILINEAR &&
+      interp != XRS_INTERP_TRIANGULAR) {
+    xrs_set_error("interp_methods must be one of 0, 1, 'nearest', 'bilinear', 'triangular'");
+    return XRS_ERR_NOTIMPL;
+  }
+  if (!ij || !src || !dst || dst_h < 1 || dst_w < 1 || n < 1 || src_h < 1 || src_w < 1 ||
+      src_sy < src_w || dst_sn < dst_h * dst_w) {
+    xrs_set_error("xrs_rectify_var: invalid argument");
+    return XRS_ERR_ARG;
+  }
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const int nb = grid_blocks(dst_h * dst_w, kThreads, 256 * 8);
+  return dispatch_dtype(src_dtype, [&](auto tag) -> int {
+    using T = decltype(tag);
+    const T* s = static_cast<const T*>(src);
+    T* d = static_cast<T*>(dst);
+    if (interp == XRS_INTERP_NEAREST)
+      hipLaunchKernelGGL((rectify_var_kernel<T, XRS_INTERP_NEAREST>), dim3(nb), dim3(kThreads),
+                         0, st, ij, dst_h, dst_w, s, n, src_h, src_w, src_sn, src_sy, d, dst_sn, fill);
+    else if (interp == XRS_INTERP_TRIANGULAR)
+      hipLaunchKernelGGL((rectify_var_kernel<T, XRS_INTERP_TRIANGULAR>), dim3(nb), dim3(kThreads),
+                         0, st, ij, dst_h, dst_w, s, n, src_h, src_w, src_sn, src_sy, d, dst_sn, fill);
+    else
+      hipLaunchKernelGGL((rectify_var_kernel<T, XRS_INTERP_BILINEAR>), dim3(nb), dim3(kThreads),
+                         0, st, ij, dst_h, dst_w, s, n, src_h, src_w, src_sn, src_sy, d, dst_sn, fill);
+    XRS_HIP_CHECK(hipGetLastError());
+    return XRS_OK;
+  });
+}

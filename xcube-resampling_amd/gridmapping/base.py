@@ -254,18 +254,19 @@ class GridMapping(abc.ABC):
         return tuple(map(int, ij_bboxes[0]))
 
     def ij_bboxes_from_xy_bboxes(self, xy_bboxes: np.ndarray, xy_border: float = 0.0,
-                                 ij_border: int = 0, ij_bboxes: np.ndarray | None = None):
-        """base.py:565-629 — per-box source ij bbox via the K4 HIP kernel."""
+                                 ij_border: int = 0, ij_bboxes: np.ndarray | None = None,
+                                 grid: tuple[int, int] | None = None):
+        """base.py:565-629 — per-box source ij bbox via the K4 HIP kernel.
+
+        ``grid=(ntx, nty)``: the boxes are the tiles of a regular grid (engine
+        extension; enables the per-pixel tile search)."""
         from ..kernels import ij_bboxes as _k4
 
         xy_bboxes = np.asarray(xy_bboxes, dtype=np.float64)
         if ij_bboxes is None:
             ij_bboxes = np.full_like(xy_bboxes, -1, dtype=np.int64)
-        xy = self.xy_coords
-        res = _k4(xy.data[0] if _is_2d_payload(xy) else xy.values[0],
-                  xy.data[1] if _is_2d_payload(xy) else xy.values[1],
-                  xy_bboxes, xy_border, ij_border)
-        ij_bboxes[:, :] = res
+        xy = self.xy_coords.data
+        ij_bboxes[:, :] = _k4(xy[0], xy[1], xy_bboxes, xy_border, ij_border, grid=grid)
         return ij_bboxes
 
     # ---- misc ------------------------------------------------------------
@@ -343,7 +344,3 @@ class GridMapping(abc.ABC):
         return (f"{type(self).__name__}(size={self.size}, tile_size={self.tile_size}, "
                 f"xy_bbox={self.xy_bbox}, xy_res={self.xy_res}, crs={self.crs.srs}, "
                 f"is_regular={self.is_regular}, is_j_axis_up={self.is_j_axis_up})")
-
-
-def _is_2d_payload(xy: DataArray) -> bool:
-    return type(xy.data).__module__.startswith("torch")

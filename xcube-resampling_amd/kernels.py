@@ -95,8 +95,113 @@ def _np_dtype(t) -> np.dtype:
     return numpy_dtype(t.dtype)
 
 
-def ij_bboxes(x_image, y_image, xy_bboxes, xy_border, ij_border):  # K4 (rectify path)
-    raise NotImplementedError("ij_bboxes kernel not built yet")
+TILE_INFO_DTYPE = np.dtype([("r0", np.int32), ("c0", np.int32), ("th", np.int32),
+                            ("tw", np.int32), ("si0", np.int32), ("sj0", np.int32),
+                            ("swin", np.int32), ("shin", np.int32), ("x_off", np.float64),
+                            ("y_off", np.float64)])
+
+
+def ij_bboxes(x_image, y_image, xy_bboxes, xy_border: float = 0.0, ij_border: int = 0,
+              grid: tuple[int, int] | None = None, device=None, stream=None) -> np.ndarray:
+    """K4 — gridmapping/bboxes.py:28-106 (compute_ij_bboxes) on the device.
+
+    x_image, y_image: (h, w) source coordinates (numpy or device tensors).
+    grid: (ntx, nty) when the boxes are the tiles of a regular grid (box k =
+    ty*ntx + tx); enables the per-pixel candidate search over tile columns and
+    rows instead of testing every box.
+    Returns the (n, 4) int64 ij bboxes [i_min, j_min, i_max, j_max] (-1 = none).
+    """
+    device = require_device(device if device is not None else getattr(x_image, "device", None))
+    x = to_device(x_image, device, np.float64)
+    y = to_device(y_image, device, np.float64)
+    h, w = x.shape
+    boxes = np.asarray(xy_bboxes, dtype=np.float64).reshape(-1, 4)
+    n = boxes.shape[0]
+    # bboxes.py:60-63 (the border is applied to every box before comparing)
+    b = np.stack([boxes[:, 0] - xy_border, boxes[:, 1] - xy_border,
+                  boxes[:, 2] + xy_border, boxes[:, 3] + xy_border], axis=1)
+    ntx = nty = 0
+    if grid is not None:
+        ntx, nty = grid
+        bb = b.reshape(nty, ntx, 4)
+        if ntx * nty == n and np.all(bb[:, :, [0, 2]] == bb[:1, :, [0, 2]]) and \
+                np.all(bb[:, :, [1, 3]] == bb[:, :1, [1, 3]]):
+            bx = to_device(np.ascontiguousarray(bb[0, :, [0, 2]].T), device)
+            by = to_device(np.ascontiguousarray(bb[:, 0, [1, 3]]), device)
+        else:
+            ntx = nty = 0
+    if ntx == 0:
+        bx = to_device(np.ascontiguousarray(b), device)
+        by = bx
+    acc = torch().tensor(np.tile(np.array([[2**31 - 1, 2**31 - 1, -1, -1]], np.int32), (n, 1)),
+                         device=device)
+    rc = _native.lib().xrs_ij_bboxes(ptr(x), ptr(y), h, w, x.stride(0), n, ntx, nty, ptr(bx),
+                                     ptr(by), ptr(acc), stream_handle(device, stream))
+    _native.check(rc, "xrs_ij_bboxes")
+    acc = acc.cpu().numpy().astype(np.int64)
+    out = np.full((n, 4), -1, dtype=np.int64)
+    found = acc[:, 2] >= 0
+    out[found] = np.stack([acc[found, 0], acc[found, 1], acc[found, 2] + 1, acc[found, 3] + 1],
+                          axis=1)
+    if ij_border != 0:  # bboxes.py:90-106
+        f = out[:, 0] != -1
+        out[f, 0] = np.maximum(out[f, 0] - ij_border, 0)
+        out[f, 1] = np.maximum(out[f, 1] - ij_border, 0)
+        out[f, 2] = np.minimum(out[f, 2] + ij_border, w)
+        out[f, 3] = np.minimum(out[f, 3] + ij_border, h)
+    return out
+
+
+def rectify_ij(x_image, y_image, tiles: np.ndarray, ntiles_x: int, dst_h: int, dst_w: int,
+               x_scale: float, y_scale: float, uv_delta: float, device=None, stream=None):
+    """K5 — per target pixel the fractional source (i, j) (rectify.py:373-576).
+
+    tiles: structured array of TILE_INFO_DTYPE (row-major tile order).
+    Returns a device tensor (2, dst_h, dst_w) float64 (NaN = no source pixel).
+    """
+    device = require_device(device)
+    x = to_device(x_image, device, np.float64)
+    y = to_device(y_image, device, np.float64)
+    h, w = x.shape
+    tiles = np.ascontiguousarray(tiles, dtype=TILE_INFO_DTYPE)
+    nq = np.where(tiles["si0"] >= 0,
+                  np.maximum(tiles["swin"].astype(np.int64) - 1, 0)
+                  * np.maximum(tiles["shin"].astype(np.int64) - 1, 0), 0)
+    per = 256
+    nch = (nq + per - 1) // per
+    chunk_tile = np.repeat(np.arange(len(tiles), dtype=np.int64), nch)
+    chunk_q0 = (np.concatenate([np.arange(k, dtype=np.int64) for k in nch]) * per
+                if len(nch) else np.zeros(0, np.int64))
+    t_dev = torch().from_numpy(tiles.view(np.uint8).copy()).to(device)
+    ct = to_device(chunk_tile if chunk_tile.size else np.zeros(1, np.int64), device)
+    cq = to_device(chunk_q0 if chunk_q0.size else np.zeros(1, np.int64), device)
+    keys = torch().empty((dst_h, dst_w), dtype=torch().int32, device=device)
+    ij = torch().empty((2, dst_h, dst_w), dtype=torch().float64, device=device)
+    rc = _native.lib().xrs_rectify_ij(ptr(x), ptr(y), h, w, x.stride(0), ptr(t_dev), len(tiles),
+                                      ntiles_x, ptr(ct), ptr(cq), int(chunk_tile.size), dst_h,
+                                      dst_w, float(x_scale), float(y_scale), float(uv_delta),
+                                      ptr(keys), ptr(ij), stream_handle(device, stream))
+    _native.check(rc, "xrs_rectify_ij")
+    return ij
+
+
+def rectify_var(ij, src, interp: str, fill, stream=None):
+    """K6 — sample one variable (n, H, W) at the fractional source positions
+    `ij` (2, H', W') (rectify.py:605-734).  Returns (n, H', W') in src dtype."""
+    device = src.device
+    code = _native.INTERP_CODES.get(interp)
+    if code is None:
+        raise NotImplementedError(
+            f"interp_methods must be one of 0, 1, 'nearest', 'bilinear', "
+            f"'triangular', was '{interp}'.")
+    n, h, w = src.shape
+    _, dh, dw = ij.shape
+    out = torch().empty((n, dh, dw), dtype=src.dtype, device=device)
+    rc = _native.lib().xrs_rectify_var(ptr(ij), dh, dw, ptr(src), _native.DTYPE_CODES[_np_dtype(src)],
+                                       n, h, w, src.stride(0), src.stride(1), ptr(out), dh * dw,
+                                       code, float(fill), stream_handle(device, stream))
+    _native.check(rc, "xrs_rectify_var")
+    return out
 
 
 _WORKSPACES: dict = {}

@@ -1,0 +1,181 @@
+"""Irregular (2-D coordinates) -> regular grid (reference: rectify.py).
+
+Host side restates ``rectify_dataset`` (rectify.py:54-179),
+``_transform_coords`` (182-231), ``_downscale_source_dataset`` (234-260),
+``_rectify_data_array`` (263-309) and the tiling math of
+``_compute_target_source_ij`` (312-370, incl. the empirical ``xy_border``)
+and ``_compute_target_source_ij_block`` (373-419: per-tile source window and
+target offsets).  The pixel work runs on the device:
+
+* K4 ``xrs_ij_bboxes``   per target tile, the source pixel bbox (numba
+                         compute_ij_bboxes, gridmapping/bboxes.py:28-106);
+* K5 ``xrs_rectify_ij``  per target pixel, the fractional source (i, j) of the
+                         first source quad that covers it (numba kernels,
+                         rectify.py:424-576) — computed once, shared by all
+                         variables, and kept in HBM;
+* K6 ``xrs_rectify_var`` per variable, sampling at those positions
+                         (rectify.py:605-734).
+"""
+
+from __future__ import annotations
+
+from collections.abc import Iterable
+
+import numpy as np
+
+from . import kernels
+from .affine import resample_dataset
+from .constants import SCALE_LIMIT, UV_DELTA
+from .crs import Transformer
+from .dataset import DataArray, Dataset
+from .device import is_device_array, require_device, to_device
+from .gridmapping import GridMapping
+from .gridmapping.helpers import chunk_sizes
+from .utils import (
+    _get_fill_value,
+    _get_interp_method_str,
+    _is_equal_crs,
+    _prep_interp_methods_downscale,
+    _select_variables,
+    as_dataset,
+    normalize_grid_mapping,
+)
+
+
+def rectify_dataset(source_ds, target_gm: GridMapping | None = None,
+                    source_gm: GridMapping | None = None,
+                    variables: str | Iterable[str] | None = None, interp_methods=None,
+                    agg_methods=None, recover_nans=False, fill_values=None,
+                    tile_size=None) -> Dataset:
+    """Rectify a dataset with 2-D coordinates onto a regular grid
+    (rectify.py:54-179; same arguments, defaults and errors)."""
+    source_ds = as_dataset(source_ds)
+    if source_gm is None:
+        source_gm = GridMapping.from_dataset(source_ds)
+    source_ds = normalize_grid_mapping(source_ds, source_gm)
+    if target_gm is None:
+        target_gm = source_gm.to_regular(tile_size=tile_size)
+    if not _is_equal_crs(source_gm, target_gm):
+        source_ds = _transform_coords(source_ds, source_gm, target_gm)
+        source_gm = GridMapping.from_dataset(source_ds)
+    source_ds = _select_variables(source_ds, variables)
+    source_ds, source_gm = _downscale_source_dataset(
+        source_ds, source_gm, target_gm, interp_methods, agg_methods, recover_nans)
+
+    target_source_ij = _compute_target_source_ij(source_gm, target_gm, UV_DELTA)
+
+    x_name, y_name = source_gm.xy_var_names
+    coords = {k: v for k, v in source_ds.coords.items() if k not in (x_name, y_name)}
+    tx_name, ty_name = target_gm.xy_var_names
+    target_coords = target_gm.to_coords()
+    coords[tx_name] = target_coords[tx_name]
+    coords[ty_name] = target_coords[ty_name]
+    coords["spatial_ref"] = DataArray(np.array(0), (), target_gm.crs.to_cf())
+    target_ds = Dataset(coords=coords, attrs=source_ds.attrs)
+
+    yx_dims = (source_gm.xy_dim_names[1], source_gm.xy_dim_names[0])
+    for var_name, data_array in source_ds.data_vars.items():
+        if data_array.dims[-2:] == yx_dims:
+            assert len(data_array.dims) in (2, 3), \
+                f"Data variable {var_name} has {len(data_array.dims)} dimensions."
+            target_ds[var_name] = _rectify_data_array(
+                data_array, var_name, target_gm, target_source_ij, interp_methods, fill_values)
+        elif yx_dims[0] not in data_array.dims and yx_dims[1] not in data_array.dims:
+            target_ds[var_name] = data_array
+    return target_ds
+
+
+def _transform_coords(source_ds: Dataset, source_gm: GridMapping,
+                      target_gm: GridMapping) -> Dataset:
+    """rectify.py:182-231 — 2-D source coordinates into the target CRS."""
+    tr = Transformer.from_crs(source_gm.crs, target_gm.crs, always_xy=True)
+    xx, yy = tr.transform(source_gm.x_coords.values, source_gm.y_coords.values)
+    source_ds = source_ds.drop_vars(source_gm.xy_var_names)
+    yx_dims = (source_gm.xy_dim_names[1], source_gm.xy_dim_names[0])
+    names = ("lon", "lat") if target_gm.crs.is_geographic else ("transformed_x", "transformed_y")
+    return source_ds.assign_coords({
+        "spatial_ref": DataArray(np.array(0), (), target_gm.crs.to_cf()),
+        names[0]: DataArray(xx, yx_dims),
+        names[1]: DataArray(yy, yx_dims),
+    })
+
+
+def _downscale_source_dataset(source_ds, source_gm: GridMapping, target_gm: GridMapping,
+                              interp_methods, agg_methods, recover_nans):
+    """rectify.py:234-260."""
+    x_scale = source_gm.x_res / target_gm.x_res
+    y_scale = source_gm.y_res / target_gm.y_res
+    if x_scale < SCALE_LIMIT or y_scale < SCALE_LIMIT:
+        w, h = round(x_scale * source_gm.width), round(y_scale * source_gm.height)
+        downscaled_size = (w if w >= 2 else 2, h if h >= 2 else 2)
+        source_ds = resample_dataset(
+            source_ds, ((1 / x_scale, 0, 0), (0, 1 / y_scale, 0)),
+            (source_gm.xy_dim_names[1], source_gm.xy_dim_names[0]), downscaled_size,
+            source_gm.tile_size, _prep_interp_methods_downscale(interp_methods), agg_methods,
+            recover_nans)
+        source_gm = GridMapping.from_dataset(source_ds)
+    return source_ds, source_gm
+
+
+def rectify_tiles(source_gm: GridMapping, target_gm: GridMapping, uv_delta: float = UV_DELTA):
+    """Host tiling of rectify.py:312-419: xy_border, per-tile source bboxes
+    (K4), per-tile source windows and target offsets (TILE_INFO records)."""
+    dst_w, dst_h = target_gm.width, target_gm.height
+    tw, th = target_gm.tile_width, target_gm.tile_height
+    dst_x_min, dst_y_min, dst_x_max, dst_y_max = target_gm.xy_bbox
+    dst_x_res, dst_y_res = target_gm.xy_res
+    j_up = target_gm.is_j_axis_up
+    num_tiles_x = dst_w / tw
+    num_tiles_y = dst_h / th
+    xy_border = min(min(2 * num_tiles_x * target_gm.x_res, 2 * num_tiles_y * target_gm.y_res),
+                    min(0.5 * (dst_x_max - dst_x_min), 0.5 * (dst_y_max - dst_y_min)))
+    ys = chunk_sizes(dst_h, th)
+    xs = chunk_sizes(dst_w, tw)
+    src_ij_bboxes = source_gm.ij_bboxes_from_xy_bboxes(
+        target_gm.xy_bboxes, xy_border=xy_border, ij_border=1, grid=(len(xs), len(ys)))
+    tiles = np.zeros(len(ys) * len(xs), dtype=kernels.TILE_INFO_DTYPE)
+    r0s = np.repeat(np.concatenate([[0], np.cumsum(ys)[:-1]]), len(xs))
+    c0s = np.tile(np.concatenate([[0], np.cumsum(xs)[:-1]]), len(ys))
+    tiles["r0"], tiles["c0"] = r0s, c0s
+    tiles["th"], tiles["tw"] = np.repeat(ys, len(xs)), np.tile(xs, len(ys))
+    i_min, j_min, i_max, j_max = (src_ij_bboxes[:, k] for k in range(4))
+    none = i_min == -1
+    tiles["si0"] = np.where(none, -1, i_min)
+    tiles["sj0"] = np.where(none, -1, j_min)
+    tiles["swin"] = np.where(none, 0, np.minimum(i_max + 1, source_gm.width) - i_min)
+    tiles["shin"] = np.where(none, 0, np.minimum(j_max + 1, source_gm.height) - j_min)
+    # rectify.py:402-406 (python float arithmetic, element by element)
+    tiles["x_off"] = [dst_x_min + int(c0) * dst_x_res for c0 in c0s]
+    tiles["y_off"] = [(dst_y_min + int(r0) * dst_y_res) if j_up else (dst_y_max - int(r0) * dst_y_res)
+                      for r0 in r0s]
+    return tiles, len(xs), src_ij_bboxes, xy_border
+
+
+def _compute_target_source_ij(source_gm: GridMapping, target_gm: GridMapping,
+                              uv_delta: float):
+    """rectify.py:312-370 -> device tensor (2, H', W') float64 (K5)."""
+    tiles, ntx, _, _ = rectify_tiles(source_gm, target_gm, uv_delta)
+    xy = source_gm.xy_coords.data
+    dst_y_scale = target_gm.y_res if target_gm.is_j_axis_up else -target_gm.y_res
+    return kernels.rectify_ij(xy[0], xy[1], tiles, ntx, target_gm.height, target_gm.width,
+                              target_gm.x_res, dst_y_scale, uv_delta)
+
+
+def _rectify_data_array(data_array: DataArray, var_name, target_gm: GridMapping,
+                        target_source_ij, interp_methods, fill_values) -> DataArray:
+    """rectify.py:263-309 (K6, one launch for all dim-0 slices)."""
+    fill_value = _get_fill_value(fill_values, var_name, data_array)
+    interp_method = _get_interp_method_str(interp_methods, var_name, data_array)
+    device = require_device()
+    on_device = is_device_array(data_array.data)
+    src = to_device(data_array.data, device)
+    expanded = src.dim() == 2
+    if expanded:
+        src = src.unsqueeze(0)
+    out = kernels.rectify_var(target_source_ij, src, interp_method, fill_value)
+    if expanded:
+        out = out[0]
+        dims = (target_gm.xy_dim_names[1], target_gm.xy_dim_names[0])
+    else:
+        dims = (data_array.dims[0], target_gm.xy_dim_names[1], target_gm.xy_dim_names[0])
+    return DataArray(out if on_device else out.cpu().numpy(), dims, data_array.attrs)
