@@ -55,9 +55,12 @@ def require_device(device=None):
             "xcube_resampling_amd: no HIP device available; the engine runs only "
             "on AMD GPUs (MI355X / gfx950) and has no CPU fallback"
         )
-    if device is None:
-        return t.device("cuda", t.cuda.current_device())
-    return t.device(device)
+    if device is not None:
+        device = t.device(device) if not isinstance(device, t.device) else device
+        if device.type == "cuda":
+            return device
+    # host arrays (numpy's ``.device`` is "cpu") run on the current HIP device
+    return t.device("cuda", t.cuda.current_device())
 
 
 def to_device(x, device, dtype=None):
