@@ -49,16 +49,21 @@ def workload(size: int, tile: int):
     return src_gm, tgm, plan, lon, lat
 
 
-def source_pixels_read(plan) -> int:
-    """Distinct in-bounds source pixels the bilinear gather reads (separable
-    plan: |rows read| x |cols read|); the algorithmic read bytes are 4x this."""
+def source_pixels_read(plan, band=None) -> int:
+    """Distinct in-bounds source pixels the bilinear gather reads for target
+    rows `band` (default all; separable plan: |rows read| x |cols read|); the
+    algorithmic read bytes are 4x this."""
     ntx, nty = plan.num_tiles
+    b0, b1 = band if band is not None else (0, plan.dst_height)
     cols = np.zeros(plan.src_width, bool)
     rows = np.zeros(plan.src_height, bool)
     for t in range(ntx * nty):
         ty, tx = divmod(t, ntx)
         c = np.arange(tx * plan.tile_width, min(plan.dst_width, (tx + 1) * plan.tile_width))
-        r = np.arange(ty * plan.tile_height, min(plan.dst_height, (ty + 1) * plan.tile_height))
+        r = np.arange(max(b0, ty * plan.tile_height),
+                      min(b1, plan.dst_height, (ty + 1) * plan.tile_height))
+        if r.size == 0:
+            continue
         ix = (plan.src_x[c] - np.float64(plan.tile_x0[t])) / plan.x_res
         iy = (plan.src_y[r] - np.float64(plan.tile_y0[t])) / -plan.y_res
         for idx, base, n, mask in ((ix, plan.tile_win[t, 0], plan.src_width, cols),
@@ -133,6 +138,10 @@ def main():
     ap.add_argument("--out-dtype", choices=["f32", "f64"], default="f32")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--shard", choices=["slices", "bands"], default="slices",
+                    help="slices: rank r reprojects slice r of an (N, S, S) cube (weak); "
+                         "bands: the ranks split the target tile rows of ONE SxS raster, "
+                         "each holding only the source rows its band reads (strong)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
     args = ap.parse_args()
 
@@ -140,10 +149,9 @@ def main():
     import torch.distributed as dist
 
     from xcube_resampling_amd import kernels
+    from xcube_resampling_amd.sharding import band_shard, env_rank, max_over_ranks
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    rank, world, local_rank = env_rank()
     torch.cuda.set_device(local_rank)
     device = torch.device("cuda", local_rank)
     if world > 1:
@@ -154,14 +162,20 @@ def main():
     out_np = np.float32 if args.out_dtype == "f32" else np.float64
     gen = torch.Generator(device=device)
     gen.manual_seed(20250905 + rank)
-    src = torch.rand((1, args.size, args.size), generator=gen, device=device, dtype=torch.float32)
-    out = torch.empty((1, args.size, args.size), device=device,
+    if args.shard == "bands":
+        shard = band_shard(plan, world, rank)
+        rows, (j0, j1) = shard.rows, shard.src_rows
+    else:
+        rows, (j0, j1) = (0, plan.dst_height), (0, plan.src_height)
+    src = torch.rand((1, j1 - j0, args.size), generator=gen, device=device, dtype=torch.float32)
+    out = torch.empty((1, rows[1] - rows[0], args.size), device=device,
                       dtype=torch.float32 if args.out_dtype == "f32" else torch.float64)
     flags = kernels.ErrorFlags(device)
 
     def step():
-        kernels.reproject(src, plan, "bilinear", float("nan"), out_dtype=out_np, out=out,
-                          flags=flags)
+        if rows[1] > rows[0]:
+            kernels.reproject(src, plan, "bilinear", float("nan"), out_dtype=out_np, out=out,
+                              rows=rows, src_row0=j0, flags=flags)
 
     for _ in range(args.warmup):
         step()
@@ -187,24 +201,23 @@ def main():
 
     elapsed = t1 - t0
     kernel_ms = ev0.elapsed_time(ev1) / args.steps
-    if world > 1:
-        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(elapsed, device)
     ms_per_step = elapsed / args.steps * 1e3
     npx = args.size * args.size
-    value = world * npx / (ms_per_step / 1e3) / 1e6
+    n_rasters = world if args.shard == "slices" else 1
+    value = n_rasters * npx / (ms_per_step / 1e3) / 1e6
 
     if rank == 0:
-        s_read = source_pixels_read(plan)
-        out_bytes = npx * np.dtype(out_np).itemsize
+        s_read = source_pixels_read(plan, rows)
+        out_bytes = (rows[1] - rows[0]) * args.size * np.dtype(out_np).itemsize
         alg_bytes = out_bytes + 4 * s_read
         achieved = alg_bytes / (kernel_ms / 1e3) / 1e9
         traffic = None
         if os.path.exists(args.traffic_json):
             with open(args.traffic_json) as f:
                 tj = json.load(f)
-            if tj.get("size") == args.size and tj.get("out_dtype") == args.out_dtype:
+            if tj.get("size") == args.size and tj.get("out_dtype") == args.out_dtype \
+                    and args.shard == "slices":
                 traffic = tj.get("hbm_bytes_per_launch")
         res = {
             "metric": "Mpixels/s reproject bilinear 40960² f32; achieved HBM GB/s vs peak",
@@ -215,20 +228,22 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "weak" if args.shard == "slices" else "strong",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic",
             "config": {
                 "workload": f"reproject EPSG:4326->EPSG:3857 bilinear {args.size}x{args.size} "
                             f"f32 source, {args.tile}x{args.tile} target tiles (configs[4]); "
-                            f"{world} slice(s) of an (N,{args.size},{args.size}) cube, 1 per GPU",
+                            + (f"{world} slice(s) of an (N,{args.size},{args.size}) cube, 1 per GPU"
+                               if args.shard == "slices" else
+                               f"one raster split into {world} tile-row band(s), 1 per GPU"),
                 "source_dtype": "f32",
                 "out_dtype": args.out_dtype,
                 "interp": "bilinear",
                 "tiles": plan.num_tiles[0] * plan.num_tiles[1],
                 "window": [plan.win_height, plan.win_width],
-                "parallelism": f"slices{world}",
+                "parallelism": f"{args.shard}{world}",
             },
             "roofline": {
                 "bound": "hbm",

@@ -1,0 +1,116 @@
+"""Multi-process (gloo, world_size 2) tests of the multi-GPU partition on the
+CPU: the row-band shard of a reprojection reads only its source rows and the
+bands reassemble to the reference's output bit for bit; dim-0 slice shards
+cover the cube exactly once; the bench's max-over-ranks clock.
+
+The per-rank compute here is the oracle (tests may use it as the checker);
+on the GPU the same partition drives xrs_reproject (test_reproject_gpu.py::
+test_row_band_sharding_matches_whole_raster)."""
+
+from __future__ import annotations
+
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from helpers import load_golden, reproject_golden_inputs
+
+POISON = np.float32(1.0e30)
+
+
+def _plan(g):
+    import xcube_resampling_amd as xrs
+
+    ds, tgm = reproject_golden_inputs(g)
+    sgm = xrs.GridMapping.from_dataset(ds)
+    return xrs.plan_reproject(sgm, tgm, xrs.Transformer.from_crs(tgm.crs, sgm.crs,
+                                                                  always_xy=True))
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 4, 8])
+def test_band_shards_partition_target_rows(world):
+    from xcube_resampling_amd.sharding import band_shard
+
+    plan = _plan(load_golden("reproject_f32.npz"))
+    shards = [band_shard(plan, world, r) for r in range(world)]
+    rows = [r for s in shards for r in range(s.row0, s.row1)]
+    assert rows == list(range(plan.dst_height))
+    for s in shards:
+        if s.row1 > s.row0:
+            assert s.row0 % plan.tile_height == 0
+            assert (s.src_row0, s.src_row1) == plan.source_rows_for(s.row0, s.row1)
+
+
+@pytest.mark.parametrize("n,world", [(1, 1), (8, 8), (5, 2), (3, 4), (17, 8)])
+def test_slice_shards_cover_cube_once(n, world):
+    from xcube_resampling_amd.sharding import slice_shard
+
+    got = [i for r in range(world) for i in range(*slice_shard(n, world, r))]
+    assert got == list(range(n))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _rank_main(rank, world, port, result_dir):
+    import sys
+
+    import torch
+    import torch.distributed as dist
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    for p in (here, os.path.dirname(here)):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    from oracle import gridmapping_ref as gref
+    from oracle import reproject_ref
+    from xcube_resampling_amd.sharding import band_shard, gather_rows, max_over_ranks
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        g = load_golden("reproject_f32.npz")
+        plan = _plan(g)
+        shard = band_shard(plan, world, rank)
+        # the rank holds only its source rows: everything else is poison
+        data = np.full_like(g["data"], POISON)
+        j0, j1 = shard.src_rows
+        data[:, j0:j1] = g["data"][:, j0:j1]
+        tsize = tuple(int(v) for v in g["tsize"])
+        ttile = tuple(int(v) for v in g["ttile"])
+        geo = gref.regular_geometry(tsize, tuple(g["txy_min"]), tuple(g["tres"]),
+                                    tile_size=ttile)
+        ntx = plan.num_tiles[0]
+        tiles = [(j, i) for j in range(shard.row0 // ttile[1], -(-shard.row1 // ttile[1]))
+                 for i in range(ntx)]
+        full = reproject_ref.reproject_array(
+            data, gref.webmerc_inverse, lambda *b: gref.transform_bounds(gref.webmerc_inverse, *b),
+            g["src_lon"], g["src_lat"], float(g["x_res"]), float(g["y_res"]), geo["x_coords"],
+            geo["y_coords"], geo["xy_bboxes"], ttile[0], ttile[1], "bilinear",
+            g["fill"].item(), tiles=tiles)
+        local = torch.from_numpy(np.ascontiguousarray(full[:, shard.row0:shard.row1]))
+        out = gather_rows(local, plan.dst_height)
+        clock = max_over_ranks(1.0 + rank)
+        if rank == 0:
+            np.save(os.path.join(result_dir, "bands.npy"), out.numpy())
+            with open(os.path.join(result_dir, "clock.txt"), "w") as f:
+                f.write(repr(clock))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_band_sharded_reprojection_matches_reference(tmp_path):
+    import torch.multiprocessing as mp
+
+    world = 2
+    mp.spawn(_rank_main, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    g = load_golden("reproject_f32.npz")
+    got = np.load(tmp_path / "bands.npy")
+    assert got.dtype == np.float64
+    np.testing.assert_array_equal(got.view(np.uint64), g["out_bilinear"].view(np.uint64))
+    assert float((tmp_path / "clock.txt").read_text()) == float(world)
