@@ -1,0 +1,272 @@
+"""Secondary measurement lines: BASELINE.json configs 1-4.
+
+    python scripts/bench_configs.py [--configs 1,2,3,4] [--steps K] [--cpu-seconds S]
+
+bench.py measures the headline metric (config 5 on one GPU per slice); this
+script measures the other configurations the same way — inputs resident in
+HBM, HIP events on the launch stream around K timed launches after a warm-up,
+algorithmic bytes per SURVEY.md §8(d) — and times the oracle on a bounded
+sample of the same workload beside it.  One JSON line per config.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+HBM_PEAK_GBS = 8000.0
+
+
+def _timed(fn, steps, warmup):
+    import torch
+
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(steps):
+        fn()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) / steps * 1e3
+    return e0.elapsed_time(e1) / steps, wall
+
+
+def _line(cfg, workload, npx, ms, wall_ms, alg_bytes, kernel, cpu, extra=None):
+    achieved = alg_bytes / (ms / 1e3) / 1e9
+    d = {"config": cfg, "workload": workload, "metric": "target Mpixels/s",
+         "value": round(npx / (wall_ms / 1e3) / 1e6, 1), "unit": "Mpixels/s",
+         "ms_per_step": round(wall_ms, 4),
+         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                      "kernel": kernel, "kernel_ms": round(ms, 4),
+                      "algorithmic_bytes": int(alg_bytes)},
+         "cpu_baseline": cpu}
+    if extra:
+        d.update(extra)
+    print(json.dumps(d), flush=True)
+
+
+def _cpu_loop(fn, seconds, unit_px):
+    px, t0 = 0, time.perf_counter()
+    while True:
+        px += fn()
+        dt = time.perf_counter() - t0
+        if dt >= seconds:
+            return px / dt / 1e6, px, dt
+
+
+# ------------------------------------------------------------------ config 1
+def config1(args):
+    """Affine nearest 1024^2 f32, EPSG:4326 -> EPSG:4326 (scale 0.9216)."""
+    import torch
+
+    import xcube_resampling_amd as xrs
+    import xcube_resampling_amd.affine as A
+    from xcube_resampling_amd import kernels
+    from oracle import affine_ref
+
+    n = 1024
+    res = 2.0 ** -10
+    lon = 10 + (np.arange(n) + 0.5) * res
+    lat = 51 - (np.arange(n) + 0.5) * res
+    sgm = xrs.GridMapping.from_coords(xrs.DataArray(lon, "lon", name="lon"),
+                                      xrs.DataArray(lat, "lat", name="lat"), "EPSG:4326")
+    tgm = xrs.GridMapping.regular((n, n), (10.1, 50.05), 0.0009, "EPSG:4326")
+    m = tgm.ij_transform_to(sgm)
+    a = np.random.default_rng(20250905).random((1, n, n), dtype=np.float32)
+    plan = A.plan_affine(a.shape, a.dtype, m, (1, n, n), (1, tgm.tile_height, tgm.tile_width),
+                         0, "first", False, np.nan)
+    src = torch.from_numpy(a).cuda()
+    out = kernels.affine(src, plan)
+    ref = affine_ref.resample_array(a, m, (1, n, n), (1, tgm.tile_height, tgm.tile_width), 0,
+                                    "first", False, np.nan)
+    assert np.array_equal(out.cpu().numpy(), ref, equal_nan=True), "config 1 parity"
+    ms, wall = _timed(lambda: kernels.affine(src, plan, out), args.steps, args.warmup)
+    s_read = n * n  # every source pixel is read at most once (scale < 1)
+    cpu_v, px, dt = _cpu_loop(lambda: affine_ref.resample_array(
+        a, m, (1, n, n), (1, n, n), 0, "first", False, np.nan).size, args.cpu_seconds, n * n)
+    _line(1, "affine nearest 1024x1024 f32 EPSG:4326 (scale 0.9216, offset 102.4 px)", n * n,
+          ms, wall, 4 * n * n + 4 * s_read, "affine_kernel<float,float,0,false>",
+          dict(value=round(cpu_v, 2), unit="Mpixels/s", cores=1, kind="port",
+               sample=f"{px // (n * n)} full 1024^2 passes in {dt:.1f} s "
+                      "(dask-image chunk restatement calling scipy.ndimage.affine_transform)"))
+
+
+# ------------------------------------------------------------------ config 2
+def config2(args):
+    """Reproject bilinear 8192^2 f32 EPSG:4326 -> EPSG:3857, 2048^2 tiles."""
+    import torch
+
+    import bench
+    from xcube_resampling_amd import kernels
+
+    size = 8192
+    src_gm, tgm, plan, lon, lat = bench.workload(size, 2048)
+    src = torch.rand((1, size, size), device="cuda", dtype=torch.float32)
+    out = torch.empty((1, size, size), device="cuda", dtype=torch.float64)
+    flags = kernels.ErrorFlags(src.device)
+    ms, wall = _timed(lambda: kernels.reproject(src, plan, "bilinear", float("nan"),
+                                                out=out, flags=flags), args.steps, args.warmup)
+    flags.raise_if_set("config 2")
+    s_read = bench.source_pixels_read(plan)
+    cpu = bench.cpu_baseline(plan, src_gm, lon, lat, tgm, args.cpu_seconds)
+    _line(2, "reproject bilinear 8192x8192 f32 EPSG:4326->EPSG:3857, 2048^2 tiles, f64 out "
+             "(the reference's bilinear dtype)", size * size, ms, wall,
+          8 * size * size + 4 * s_read, "gather_separable_mlp_kernel<float,double,1,4>", cpu)
+
+
+# ------------------------------------------------------------------ config 3
+def config3(args):
+    """Coarsen mean 4x4: 16384^2 f32 -> 4096^2 (bilinear upscale at scale 1 + nanmean)."""
+    import torch
+
+    import xcube_resampling_amd as xrs
+    import xcube_resampling_amd.affine as A
+    from xcube_resampling_amd import kernels
+    from oracle import affine_ref
+
+    n, k = 16384, 4
+    res = 2.0 ** -10
+    lon = (np.arange(n) + 0.5) * res
+    lat = n * res - (np.arange(n) + 0.5) * res
+    sgm = xrs.GridMapping.from_coords(xrs.DataArray(lon, "lon", name="lon"),
+                                      xrs.DataArray(lat, "lat", name="lat"), "EPSG:4326")
+    tgm = xrs.GridMapping.regular((n // k, n // k), (0, 0), res * k, "EPSG:4326")
+    m = tgm.ij_transform_to(sgm)
+    assert m == ((4.0, 0.0, 0.0), (0.0, 4.0, 0.0)), m
+    g = torch.Generator(device="cuda")
+    g.manual_seed(20250905)
+    src = torch.rand((1, n, n), generator=g, device="cuda", dtype=torch.float32)
+    oc = (1, tgm.tile_height, tgm.tile_width)
+    plan = A.plan_affine(tuple(src.shape), np.dtype(np.float32), m, (1, n // k, n // k), oc, 1,
+                         "mean", False, np.nan)
+    out = kernels.affine(src, plan)
+    # parity on a corner (the oracle on the full 1 GiB raster takes minutes)
+    c = 1024
+    a = src[:, :c, :c].cpu().numpy()
+    ref = affine_ref.resample_array(a, m, (1, c // k, c // k), (1, c // k, c // k), 1, "mean",
+                                    False, np.nan)
+    assert np.array_equal(out[:, :c // k - 1, :c // k - 1].cpu().numpy(),
+                          ref[:, :-1, :-1]), "config 3 parity"
+    ms, wall = _timed(lambda: kernels.affine(src, plan, out), args.steps, args.warmup)
+    cs = 2048
+    sample = src[:, :cs, :cs].cpu().numpy()
+    cpu_v, px, dt = _cpu_loop(lambda: affine_ref.resample_array(
+        sample, m, (1, cs // k, cs // k), (1, cs // k, cs // k), 1, "mean", False,
+        np.nan).size, args.cpu_seconds, 0)
+    _line(3, "coarsen mean 4x4: 16384x16384 f32 -> 4096x4096 (affine bilinear at the 4x grid "
+             "+ nanmean)", (n // k) ** 2, ms, wall, 4 * n * n + 4 * (n // k) ** 2,
+          "affine_kernel<float,float,1,false> (fused upscale+coarsen)",
+          dict(value=round(cpu_v, 3), unit="Mpixels/s", cores=1, kind="port",
+               sample=f"{px // (cs // k) ** 2} passes of a 2048^2 -> 512^2 corner in {dt:.1f} s "
+                      "(scipy affine_transform + numpy nanmean, dask chunk.coarsen order)"))
+
+
+# ------------------------------------------------------------------ config 4
+def config4(args):
+    """Rectify a 4000x4800 jittered swath to a ~8.3k x 5.4k EPSG:4326 grid, 512^2 tiles."""
+    import torch
+
+    import xcube_resampling_amd as xrs
+    from xcube_resampling_amd import kernels
+    from xcube_resampling_amd import rectify as R
+    from oracle import rectify_ref
+
+    w, h = 4000, 4800
+    rng = np.random.default_rng(20250905)
+    i = np.arange(w)[None, :].astype(np.float64)
+    j = np.arange(h)[:, None].astype(np.float64)
+    lat = 60 - 0.0027 * j - 0.0004 * i + 1e-9 * (i - 2000) ** 2 \
+        + rng.normal(0, 0.05 * 0.0027, (h, w))
+    lon = 5 + 0.0045 * i + 0.0009 * j + rng.normal(0, 0.05 * 0.0045, (h, w))
+    var = rng.random((1, h, w), dtype=np.float32)
+    res = 0.0027
+    x0, y0 = float(np.floor(lon.min() / res) * res), float(np.floor(lat.min() / res) * res)
+    tw, th = int(np.ceil((lon.max() - x0) / res)), int(np.ceil((lat.max() - y0) / res))
+    tgm = xrs.GridMapping.regular((tw, th), (x0, y0), res, "EPSG:4326", tile_size=512)
+    sgm = xrs.GridMapping.from_coords(xrs.DataArray(lon, ("y", "x"), name="lon"),
+                                      xrs.DataArray(lat, ("y", "x"), name="lat"), "EPSG:4326")
+    dlon, dlat = torch.from_numpy(lon).cuda(), torch.from_numpy(lat).cuda()
+    src = torch.from_numpy(var).cuda()
+    xy = (dlon, dlat)
+
+    tiles, ntx, bb, _ = R.rectify_tiles(sgm, tgm)
+    dst_y_scale = -tgm.y_res
+
+    def k5():
+        return kernels.rectify_ij(xy[0], xy[1], tiles, ntx, tgm.height, tgm.width, tgm.x_res,
+                                  dst_y_scale, 1e-3)
+
+    ij = k5()
+    covered = int(torch.sum(~torch.isnan(ij[0])).item())
+    k5_ms, _ = _timed(k5, args.steps, args.warmup)
+    lines = {}
+    for interp in ("nearest", "bilinear"):
+        k6_ms, _ = _timed(lambda: kernels.rectify_var(ij, src, interp, float("nan")),
+                          args.steps, args.warmup)
+        lines[interp] = k6_ms
+
+    def pipeline(interp):
+        t, n_x, _, _ = R.rectify_tiles(sgm, tgm)
+        ij_ = kernels.rectify_ij(xy[0], xy[1], t, n_x, tgm.height, tgm.width, tgm.x_res,
+                                 dst_y_scale, 1e-3)
+        return kernels.rectify_var(ij_, src, interp, float("nan"))
+
+    npx = tgm.width * tgm.height
+    S = w * h
+    for interp in ("nearest", "bilinear"):
+        ms, wall = _timed(lambda: pipeline(interp), max(3, args.steps // 4), 1)
+        cores = min(16, len(os.sched_getaffinity(0)))
+        # bounded CPU sample: a 1000x1200 sub-swath rectified onto its own bbox
+        sub = (slice(0, 1200), slice(0, 1000))
+        slon, slat = lon[sub], lat[sub]
+        sx0 = float(np.floor(slon.min() / res) * res)
+        sy0 = float(np.floor(slat.min() / res) * res)
+        ssz = (int(np.ceil((slon.max() - sx0) / res)), int(np.ceil((slat.max() - sy0) / res)))
+        sbbox = (sx0, sy0, sx0 + ssz[0] * res, sy0 + ssz[1] * res)
+
+        def cpu_once():
+            ij_c, _ = rectify_ref.compute_target_source_ij(slon, slat, ssz, (512, 512), sbbox,
+                                                           (res, res), threads=cores)
+            rectify_ref.compute_var_image(ij_c, var[:, :1200, :1000], np.nan, interp, (512, 512),
+                                          threads=cores)
+            return ssz[0] * ssz[1]
+
+        cpu_v, px, dt = _cpu_loop(cpu_once, args.cpu_seconds, 0)
+        _line(4, f"rectify {interp}: 4000x4800 jittered swath (f64 lon/lat, f32 var) -> "
+                 f"{tgm.width}x{tgm.height} EPSG:4326 res 0.0027, 512^2 tiles "
+                 "(K4 bbox + host tiling + K5 + K6, end to end)",
+              npx, ms, wall, 16 * S + 4 * S + 4 * npx,
+              f"K5 rectify_claim+resolve {k5_ms:.3f} ms, K6 {lines[interp]:.3f} ms",
+              dict(value=round(cpu_v, 2), unit="Mpixels/s", cores=cores, kind="port",
+                   sample=f"{px // (ssz[0] * ssz[1])} passes of a 1000x1200 sub-swath -> "
+                          f"{ssz[0]}x{ssz[1]} in {dt:.1f} s (C restatement of the numba "
+                          "kernels, tiles on a thread pool)"),
+              {"covered_px": covered, "k5_ms": round(k5_ms, 4),
+               "k6_ms": round(lines[interp], 4)})
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="1,2,3,4")
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    args = ap.parse_args()
+    for c in args.configs.split(","):
+        {"1": config1, "2": config2, "3": config3, "4": config4}[c.strip()](args)
+
+
+if __name__ == "__main__":
+    main()
