@@ -17,17 +17,20 @@
 //   the chunk's input slice; order 0: floor(c+0.5).  Stored as global source
 //   indices + float64 weights.  Exact: the matrix is diagonal, so every
 //   per-pixel coordinate depends on one output index only.
-// K2b/K3 affine_kernel: one 256-thread block = a 64x4 tile of output pixels.
-//   The source patch the tile needs (bounded by the monotone axis tables) is
-//   staged in LDS with coalesced loads (two slices when the zero-weight time
-//   neighbour of order-1 3-D transforms must be read), then each thread
-//   evaluates scipy's corner sum ((v*wy)*wx accumulated from +0.0 in corner
-//   order, last dim fastest) for its sub-samples and reduces them exactly like
-//   numpy's nan-reducers under dask's chunk.coarsen (row sums pairwise, rows
-//   accumulated sequentially, mean divided in float64).  Tiles whose patch
-//   does not fit the LDS budget read the corners from global memory instead.
+// K2b affine_direct_kernel (plain affine; coarsen first/last/center pick one
+//   sub-sample): one output pixel per thread, lanes on consecutive columns,
+//   scipy's corner sum ((v*wy)*wx accumulated from +0.0 in corner order, last
+//   dim fastest; the zero-weight time neighbour of order-1 3-D transforms
+//   included, as it propagates NaN) evaluated from global memory.
+// K3 affine_reduce_kernel (mean/sum/max/min/prod/count): per 64x4 output
+//   tile, the intermediate band of a group of sub-sample rows is evaluated
+//   into LDS with lanes on consecutive intermediate columns (coalesced), then
+//   each thread folds its pixel's values exactly like numpy's nan-reducers
+//   under dask's chunk.coarsen (row sums pairwise, rows accumulated
+//   sequentially, mean divided in float64).
 
 #include <cmath>
+#include <cstdlib>
 #include <limits>
 #include <type_traits>
 
@@ -39,7 +42,6 @@ namespace {
 constexpr int kThreads = 256;
 constexpr int kTileW = 64;                 // output pixels per tile row
 constexpr int kTileH = kThreads / kTileW;  // output rows per tile
-constexpr int kLdsBytes = 40 * 1024;       // patch budget per block (4 blocks / CU)
 
 struct AxisTab {   // scipy footprint of one intermediate row / column
   int32_t g0;      // global source index of the first tap; -1 = out of bounds (cval)
@@ -126,6 +128,9 @@ template <> struct ScipyOut<double> {
 template <typename T> __device__ inline bool is_nan(T v) { return false; }
 template <> __device__ inline bool is_nan<float>(float v) { return v != v; }
 template <> __device__ inline bool is_nan<double>(double v) { return v != v; }
+template <typename T> __device__ inline bool is_finite(T v) { return true; }
+template <> __device__ inline bool is_finite<float>(float v) { return v - v == 0.0f; }
+template <> __device__ inline bool is_finite<double>(double v) { return v - v == 0.0; }
 
 enum Agg : int {
   AGG_NONE = 0, AGG_MEAN = 1, AGG_SUM = 2, AGG_MAX = 3, AGG_MIN = 4, AGG_PROD = 5,
@@ -187,214 +192,312 @@ __device__ inline void store_any(void* dst, int64_t idx, int dtype, double fv, i
   }
 }
 
-// Source access: LDS patch or global memory.
+// Source access: global memory (slice t and its zero-weight time neighbour
+// t1).  The out-of-bounds marker (-1) is clamped to a valid element; eval()
+// returns cval there.
 template <typename T>
-struct Patch {
-  const T* lds0;     // slice t
-  const T* lds1;     // zero-weight time neighbour slice
-  int32_t r0, c0, w; // patch origin and row length
-  bool use_lds;
-  const T* g0;       // global slice t
-  const T* g1;       // global neighbour slice
+struct Src {
+  const T* g0;       // slice t
+  const T* g1;       // zero-weight time neighbour slice
   int64_t sy;
-  __device__ inline T at0(int32_t r, int32_t c) const {
-    return use_lds ? lds0[(r - r0) * w + (c - c0)] : g0[(int64_t)r * sy + c];
-  }
-  __device__ inline T at1(int32_t r, int32_t c) const {
-    return use_lds ? lds1[(r - r0) * w + (c - c0)] : g1[(int64_t)r * sy + c];
-  }
+  __device__ inline int32_t crow(int32_t g) const { return max(g, 0); }
+  __device__ inline int32_t ccol(int32_t g) const { return max(g, 0); }
+  __device__ inline const T* row0(int32_t r) const { return g0 + (int64_t)r * sy; }
+  __device__ inline const T* row1(int32_t r) const { return g1 + (int64_t)r * sy; }
 };
 
-// One sub-sample: scipy's value (intermediate dtype I) — recover_nans handled
-// by the caller passing RECOVER.
-template <typename T, typename I, int ORDER, bool RECOVER>
-__device__ inline I subsample(const Patch<T>& p, const AxisTab& ey, const AxisTab& ex,
-                              bool has_t1, double cval) {
-  if (ey.g0 < 0 || ex.g0 < 0) {
-    if (RECOVER) {  // im = cval cast to T, norm = cval (float64)
-      const double im = (double)ScipyOut<T>::cast(cval);
-      const double norm = cval;
-      return (fabs(norm) <= 1e-8) ? (I)NAN : (I)(im / norm);
+// The source taps of one sub-sample (loaded first, evaluated later, so that
+// several sub-samples' loads are in flight together).
+template <typename T>
+struct Taps {
+  T v0[2][2], v1[2][2];
+  // Branch-free: out-of-bounds entries (g0 == -1) read element 0 of the row /
+  // column instead (a valid address); eval() then returns cval.
+  template <int ORDER, bool HAS_T1, typename R>
+  __device__ inline void load(const R& p, const AxisTab& ey, const AxisTab& ex) {
+    const int32_t ra = p.crow(ey.g0), ca = p.ccol(ex.g0);
+    const T* r0 = p.row0(ra);
+    if (ORDER == 0) { v0[0][0] = r0[ca]; return; }
+    const int32_t rb = p.crow(ey.g1), cb = p.ccol(ex.g1);
+    const T* r1 = p.row0(rb);
+    v0[0][0] = r0[ca]; v0[0][1] = r0[cb];
+    v0[1][0] = r1[ca]; v0[1][1] = r1[cb];
+    if (HAS_T1) {
+      const T* q0 = p.row1(ra);
+      const T* q1 = p.row1(rb);
+      v1[0][0] = q0[ca]; v1[0][1] = q0[cb];
+      v1[1][0] = q1[ca]; v1[1][1] = q1[cb];
     }
-    return (I)ScipyOut<T>::cast(cval);
   }
-  if (ORDER == 0) return (I)p.at0(ey.g0, ex.g0);
-  const int32_t rr[2] = {ey.g0, ey.g1}, cc[2] = {ex.g0, ex.g1};
-  const double wy[2] = {ey.w0, ey.w1}, wx[2] = {ex.w0, ex.w1};
-  double t = 0.0, tn = 0.0;
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      const T v = p.at0(rr[a], cc[b]);
-      if (RECOVER) {
-        const double fv = is_nan(v) ? 0.0 : (double)v;
-        const double mv = is_nan(v) ? 0.0 : 1.0;
-        t += (fv * wy[a]) * wx[b];
-        tn += (mv * wy[a]) * wx[b];
-      } else {
-        t += ((double)v * wy[a]) * wx[b];
+  // scipy's value (intermediate dtype I); recover_nans when RECOVER
+  template <typename I, int ORDER, bool RECOVER, bool HAS_T1>
+  __device__ inline I eval(const AxisTab& ey, const AxisTab& ex, double cval) const {
+    if (ey.g0 < 0 || ex.g0 < 0) {
+      if (RECOVER) {  // im = cval cast to T, norm = cval (float64)
+        const double im = (double)ScipyOut<T>::cast(cval);
+        const double norm = cval;
+        return (fabs(norm) <= 1e-8) ? (I)NAN : (I)(im / norm);
       }
+      return (I)ScipyOut<T>::cast(cval);
     }
-  if (has_t1) {  // the zero-weight neighbour slice: contributes ((v*0)*wy)*wx
+    if (ORDER == 0) return (I)v0[0][0];
+    if (!RECOVER && ey.w1 == 0.0 && ex.w1 == 0.0) {
+      // Integral position (w0 = 1, w1 = 0 on both axes; every integer-factor
+      // coarsen of aligned grids): scipy's sum below reduces EXACTLY to
+      //   t = ((((+0 + v00) + (v01*1)*0) + (v10*0)*1) + (v11*0)*0) [+ t1 terms]
+      // where each zero-weight term is a signed zero, or NaN when its tap is
+      // +-inf/NaN; adding signed zeros to +0 + v00 leaves v00 except -0 -> +0.
+      bool bad = !is_finite(v0[0][1]) || !is_finite(v0[1][0]) || !is_finite(v0[1][1]);
+      if (HAS_T1)
+        bad = bad || !is_finite(v1[0][0]) || !is_finite(v1[0][1]) || !is_finite(v1[1][0]) ||
+              !is_finite(v1[1][1]);
+      const T a = v0[0][0];
+      if (bad) return (I)ScipyOut<T>::cast(NAN);
+      return (I)(a == (T)0 ? (T)0 : a);
+    }
+    const double wy[2] = {ey.w0, ey.w1}, wx[2] = {ex.w0, ex.w1};
+    double t = 0.0, tn = 0.0;
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
       for (int b = 0; b < 2; ++b) {
-        const T v = p.at1(rr[a], cc[b]);
+        const T v = v0[a][b];
         if (RECOVER) {
           const double fv = is_nan(v) ? 0.0 : (double)v;
-          t += ((fv * 0.0) * wy[a]) * wx[b];
-          tn += ((is_nan(v) ? 0.0 : 0.0) * wy[a]) * wx[b];
+          const double mv = is_nan(v) ? 0.0 : 1.0;
+          t += (fv * wy[a]) * wx[b];
+          tn += (mv * wy[a]) * wx[b];
         } else {
-          t += (((double)v * 0.0) * wy[a]) * wx[b];
+          t += ((double)v * wy[a]) * wx[b];
         }
       }
+    if (HAS_T1) {  // the zero-weight neighbour slice: contributes ((v*0)*wy)*wx
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          const T v = v1[a][b];
+          if (RECOVER) {
+            const double fv = is_nan(v) ? 0.0 : (double)v;
+            t += ((fv * 0.0) * wy[a]) * wx[b];
+            tn += (0.0 * wy[a]) * wx[b];
+          } else {
+            t += (((double)v * 0.0) * wy[a]) * wx[b];
+          }
+        }
+    }
+    if (RECOVER) {
+      const double im = (double)ScipyOut<T>::cast(t);
+      return (fabs(tn) <= 1e-8) ? (I)NAN : (I)(im / tn);
+    }
+    return (I)ScipyOut<T>::cast(t);
   }
-  if (RECOVER) {
-    const double im = (double)ScipyOut<T>::cast(t);
-    return (fabs(tn) <= 1e-8) ? (I)NAN : (I)(im / tn);
-  }
-  return (I)ScipyOut<T>::cast(t);
+};
+
+template <typename T, typename I, int ORDER, bool RECOVER, bool HAS_T1>
+__device__ inline I subsample(const Src<T>& p, const AxisTab& ey, const AxisTab& ex,
+                              double cval) {
+  Taps<T> tp;
+  tp.template load<ORDER, HAS_T1>(p, ey, ex);
+  return tp.template eval<I, ORDER, RECOVER, HAS_T1>(ey, ex, cval);
 }
 
+template <typename I>
+__device__ inline void store_value(const AffineArgs& a, int64_t didx, I v) {
+  if (std::is_floating_point<I>::value) store_any(a.dst, didx, a.dst_dtype, (double)v, 0, false);
+  else store_any(a.dst, didx, a.dst_dtype, 0.0, (int64_t)v, true);
+}
+
+__device__ inline int32_t wave_uniform(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// K2 (no reduction: plain affine, or coarsen first/last/center which pick ONE
+// sub-sample): one output pixel per thread, a 64x4 tile per block, lanes on
+// consecutive output columns (coalesced xtab reads, stores and — for scales
+// near 1 — source reads), the row entry wave-uniform (scalar loads).
 template <typename T, typename I, int ORDER, bool RECOVER>
 __global__ void __launch_bounds__(kThreads)
-affine_kernel(AffineArgs a) {
-  extern __shared__ __align__(16) unsigned char smem[];
-  T* lds = reinterpret_cast<T*>(smem);
-  __shared__ int32_t s_bounds[4];
-
-  const int tx = threadIdx.x % kTileW, ty = threadIdx.x / kTileW;
+affine_direct_kernel(AffineArgs a, const AxisTab* __restrict__ ytab,
+                     const AxisTab* __restrict__ xtab) {
+  const int tx = threadIdx.x % kTileW;
+  const int ty = wave_uniform(threadIdx.x / kTileW);
   const int64_t ntx = (a.out_w + kTileW - 1) / kTileW, nty = (a.out_h + kTileH - 1) / kTileH;
   const int64_t nwork = ntx * nty * a.nt;
   const XcdSlice sl = xcd_slice(nwork);
-  const int64_t cap = kLdsBytes / (int64_t)sizeof(T);
+  int sj = 0, si = 0;
+  if (a.agg == AGG_LAST) { sj = (int)a.dy - 1; si = (int)a.dx - 1; }
+  if (a.agg == AGG_CENTER) { sj = (int)a.dy / 2; si = (int)a.dx / 2; }
+  for (int64_t w = sl.first; w < sl.end; w += sl.step) {
+    const int64_t t = w / (ntx * nty);
+    const int64_t rem = w - t * ntx * nty;
+    const int64_t tj = rem / ntx, ti = rem - tj * ntx;
+    const int64_t oj = tj * kTileH + ty, oi = ti * kTileW + tx;
+    if (oj >= a.out_h) continue;
+    const int64_t t1 = a.t_next ? a.t_next[t] : -1;
+    Src<T> p;
+    p.g0 = static_cast<const T*>(a.src) + t * a.src_st;
+    p.g1 = t1 >= 0 ? static_cast<const T*>(a.src) + t1 * a.src_st : p.g0;
+    p.sy = a.src_sy;
+    const AxisTab ey = ytab[oj * a.dy + sj];
+    if (oi < a.out_w) {
+      const AxisTab ex = xtab[oi * a.dx + si];
+      I v;
+      if (ORDER == 1 && t1 >= 0) v = subsample<T, I, ORDER, RECOVER, true>(p, ey, ex, a.cval);
+      else v = subsample<T, I, ORDER, RECOVER, false>(p, ey, ex, a.cval);
+      store_value<I>(a, t * a.dst_st + oj * a.dst_sy + oi, v);
+    }
+  }
+}
+
+// LDS position of intermediate column k of a tile row: one pad word every 32
+// so the reduce pass (lane tx reads k = tx*dx + si) is bank-conflict free.
+__device__ inline int lds_pos(int k) { return k + (k >> 5); }
+
+// K3 (coarsen reducers): a block owns 64 output columns x kRedRows output
+// rows.  For each group of G sub-sample rows it (A) evaluates the scipy
+// sub-samples of the whole intermediate band — lanes on consecutive
+// intermediate columns, so source reads and xtab reads coalesce and the row
+// entry is block-uniform — into LDS, then (B) every thread folds its output
+// pixel's dx values of each row exactly as numpy (pairwise row sum, rows
+// accumulated sequentially).  The dy*dx intermediate never reaches HBM.
+constexpr int kRedRows = kThreads / kTileW;  // 4 output rows per block
+
+// (A) of K3: sub-samples of rows s0 .. s0+g_n-1 of every output row of the
+// tile into the LDS band.  The column entry is the same for all rows
+// (hoisted), the row entries are block-uniform (scalar loads), and the taps of
+// KB rows are loaded before any is consumed (memory-level parallelism).
+template <typename T, typename I, int ORDER, bool RECOVER, bool HAS_T1, int KB, typename R>
+__device__ inline void fill_band(const AffineArgs& a, const R& p,
+                                 const AxisTab* __restrict__ ytab,
+                                 const AxisTab* __restrict__ xtab, I* buf, int64_t oj0,
+                                 int64_t ic0, int rows, int s0, int g_n, int kmax,
+                                 int row_stride) {
+  for (int k = threadIdx.x; k < kmax; k += kThreads) {
+    const AxisTab ex = xtab[ic0 + k];
+    for (int r = 0; r < rows; ++r) {
+      const AxisTab* yrow = ytab + (oj0 + r) * a.dy + s0;
+      I* bcol = buf + (r * g_n) * row_stride + lds_pos(k);
+      for (int g0 = 0; g0 < g_n; g0 += KB) {
+        Taps<T> tp[KB];
+        AxisTab ey[KB];
+#pragma unroll
+        for (int q = 0; q < KB; ++q) {
+          ey[q] = yrow[min(g0 + q, g_n - 1)];
+          tp[q].template load<ORDER, HAS_T1, R>(p, ey[q], ex);
+        }
+#pragma unroll
+        for (int q = 0; q < KB; ++q)
+          if (g0 + q < g_n)
+            bcol[(g0 + q) * row_stride] =
+                tp[q].template eval<I, ORDER, RECOVER, HAS_T1>(ey[q], ex, a.cval);
+      }
+    }
+  }
+}
+
+template <typename T, typename I, int ORDER, bool RECOVER, int KB>
+__global__ void __launch_bounds__(kThreads)
+affine_reduce_kernel(AffineArgs a, const AxisTab* __restrict__ ytab,
+                     const AxisTab* __restrict__ xtab, int group) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  I* buf = reinterpret_cast<I*>(smem);
+  const int tx = threadIdx.x % kTileW;
+  const int ty = wave_uniform(threadIdx.x / kTileW);
+  const int ny = (int)a.dy, nx = (int)a.dx;
+  const int band_w = kTileW * nx;                 // intermediate columns per tile row
+  const int row_stride = lds_pos(band_w - 1) + 1;
+  const int64_t ntx = (a.out_w + kTileW - 1) / kTileW;
+  const int64_t nty = (a.out_h + kRedRows - 1) / kRedRows;
+  const int64_t nwork = ntx * nty * a.nt;
+  const XcdSlice sl = xcd_slice(nwork);
+  const int64_t iw = a.out_w * a.dx;
 
   for (int64_t w = sl.first; w < sl.end; w += sl.step) {
     const int64_t t = w / (ntx * nty);
     const int64_t rem = w - t * ntx * nty;
     const int64_t tj = rem / ntx, ti = rem - tj * ntx;
-    const int64_t oj0 = tj * kTileH, oi0 = ti * kTileW;
+    const int64_t oj0 = tj * kRedRows, oi0 = ti * kTileW;
+    const int rows = (int)min((int64_t)kRedRows, a.out_h - oj0);
     const int64_t t1 = a.t_next ? a.t_next[t] : -1;
-    const bool has_t1 = ORDER == 1 && t1 >= 0;
-
-    // ---- patch bounds of the tile (rows/cols of all in-bounds taps)
-    if (threadIdx.x < 4) s_bounds[threadIdx.x] = (threadIdx.x & 1) ? -1 : INT32_MAX;
-    __syncthreads();
-    {
-      int32_t rmin = INT32_MAX, rmax = -1, cmin = INT32_MAX, cmax = -1;
-      const int64_t ry0 = oj0 * a.dy, ry1 = min(a.out_h, oj0 + kTileH) * a.dy;
-      for (int64_t r = ry0 + threadIdx.x; r < ry1; r += kThreads) {
-        const AxisTab e = a.ytab[r];
-        if (e.g0 >= 0) {
-          rmin = min(rmin, min(e.g0, e.g1));
-          rmax = max(rmax, max(e.g0, e.g1));
-        }
-      }
-      const int64_t cx0 = oi0 * a.dx, cx1 = min(a.out_w, oi0 + kTileW) * a.dx;
-      for (int64_t c = cx0 + threadIdx.x; c < cx1; c += kThreads) {
-        const AxisTab e = a.xtab[c];
-        if (e.g0 >= 0) {
-          cmin = min(cmin, min(e.g0, e.g1));
-          cmax = max(cmax, max(e.g0, e.g1));
-        }
-      }
-      if (rmax >= 0) { atomicMin(&s_bounds[0], rmin); atomicMax(&s_bounds[1], rmax); }
-      if (cmax >= 0) { atomicMin(&s_bounds[2], cmin); atomicMax(&s_bounds[3], cmax); }
-    }
-    __syncthreads();
-    const int32_t pr0 = s_bounds[0], pr1 = s_bounds[1], pc0 = s_bounds[2], pc1 = s_bounds[3];
-    const bool any = pr1 >= 0 && pc1 >= 0;
-    const int64_t ph = any ? (int64_t)(pr1 - pr0 + 1) : 0, pw = any ? (int64_t)(pc1 - pc0 + 1) : 0;
-    const int64_t need = ph * pw * (has_t1 ? 2 : 1);
-
-    Patch<T> p;
+    Src<T> p;
     p.g0 = static_cast<const T*>(a.src) + t * a.src_st;
-    p.g1 = has_t1 ? static_cast<const T*>(a.src) + t1 * a.src_st : p.g0;
+    p.g1 = t1 >= 0 ? static_cast<const T*>(a.src) + t1 * a.src_st : p.g0;
     p.sy = a.src_sy;
-    p.r0 = pr0; p.c0 = pc0; p.w = (int32_t)pw;
-    p.use_lds = any && need <= cap;
-    p.lds0 = lds;
-    p.lds1 = lds + ph * pw;
-    if (p.use_lds) {  // coalesced staging: consecutive threads -> consecutive columns
-      const int64_t n1 = ph * pw;
-      for (int64_t i = threadIdx.x; i < n1; i += kThreads) {
-        const int64_t r = i / pw, c = i - r * pw;
-        lds[i] = p.g0[(int64_t)(pr0 + r) * a.src_sy + pc0 + c];
-        if (has_t1) lds[n1 + i] = p.g1[(int64_t)(pr0 + r) * a.src_sy + pc0 + c];
-      }
-    }
-    __syncthreads();
+    const int64_t ic0 = oi0 * a.dx;
+    const int kmax = (int)min((int64_t)band_w, iw - ic0);
 
-    // ---- one output pixel per thread
-    const int64_t oj = oj0 + ty, oi = oi0 + tx;
-    if (oj < a.out_h && oi < a.out_w) {
-      const int64_t didx = t * a.dst_st + oj * a.dst_sy + oi;
-      const int ny = (int)a.dy, nx = (int)a.dx;
-      if (a.agg == AGG_NONE || a.agg == AGG_FIRST || a.agg == AGG_LAST || a.agg == AGG_CENTER) {
-        int sj = 0, si = 0;
-        if (a.agg == AGG_LAST) { sj = ny - 1; si = nx - 1; }
-        if (a.agg == AGG_CENTER) { sj = ny / 2; si = nx / 2; }
-        const I v = subsample<T, I, ORDER, RECOVER>(p, a.ytab[oj * a.dy + sj],
-                                                    a.xtab[oi * a.dx + si], has_t1, a.cval);
-        if (std::is_floating_point<I>::value) store_any(a.dst, didx, a.dst_dtype, (double)v, 0, false);
-        else store_any(a.dst, didx, a.dst_dtype, 0.0, (int64_t)v, true);
-      } else if (std::is_floating_point<I>::value) {
-        // float reducers (nanmean / nansum / nanmax / nanmin / nanprod / count)
-        I total = (I)0.0, prod = (I)1.0, mx = (I)0.0;
-        int64_t cnt = 0, nonzero = 0;
-        bool have = false;
-        for (int sj = 0; sj < ny; ++sj) {
-          const AxisTab ey = a.ytab[oj * a.dy + sj];
-          auto val = [&](int si) -> I {
-            const I v = subsample<T, I, ORDER, RECOVER>(p, ey, a.xtab[oi * a.dx + si], has_t1,
-                                                        a.cval);
-            const bool nan = v != v;
-            cnt += nan ? 0 : 1;
-            nonzero += (v != (I)0.0) ? 1 : 0;
-            prod = prod * (nan ? (I)1.0 : v);
-            if (a.agg == AGG_MAX) {  // np.fmax.reduce: (acc >= v || isnan(v)) ? acc : v
-              if (!have) { mx = v; have = true; }
-              else mx = (mx >= v || nan) ? mx : v;
-            } else if (a.agg == AGG_MIN) {
-              if (!have) { mx = v; have = true; }
-              else mx = (mx <= v || nan) ? mx : v;
-            }
-            return nan ? (I)0.0 : v;
-          };
-          total = total + pairwise_row<I>(nx, val);
+    const bool two = ORDER == 1 && t1 >= 0;
+
+    // per-thread reducer state
+    I total = (I)0.0, prod = (I)1.0, mx = (I)0.0;
+    double dtotal = 0.0;
+    int64_t cnt = 0, nonzero = 0, isum = 0, iprod = 1, imx = 0;
+    bool have = false;
+
+    for (int s0 = 0; s0 < ny; s0 += group) {
+      const int g_n = min(group, ny - s0);
+      // (A) sub-samples of rows s0 .. s0+g_n-1 into the band
+      if (two)
+        fill_band<T, I, ORDER, RECOVER, true, KB>(a, p, ytab, xtab, buf, oj0, ic0, rows, s0,
+                                                  g_n, kmax, row_stride);
+      else
+        fill_band<T, I, ORDER, RECOVER, false, KB>(a, p, ytab, xtab, buf, oj0, ic0, rows, s0,
+                                                   g_n, kmax, row_stride);
+      __syncthreads();
+      // (B) fold this thread's values row by row
+      const int64_t oi = oi0 + tx;
+      if (ty < rows && oi < a.out_w) {
+        for (int g = 0; g < g_n; ++g) {
+          const I* brow = buf + (ty * g_n + g) * row_stride;
+          const int kb = tx * nx;
+          if (std::is_floating_point<I>::value) {
+            auto val = [&](int si) -> I {
+              const I v = brow[lds_pos(kb + si)];
+              const bool nan = v != v;
+              cnt += nan ? 0 : 1;
+              nonzero += (v != (I)0.0) ? 1 : 0;
+              prod = prod * (nan ? (I)1.0 : v);
+              if (a.agg == AGG_MAX) {  // np.fmax.reduce
+                if (!have) { mx = v; have = true; }
+                else mx = (mx >= v || nan) ? mx : v;
+              } else if (a.agg == AGG_MIN) {
+                if (!have) { mx = v; have = true; }
+                else mx = (mx <= v || nan) ? mx : v;
+              }
+              return nan ? (I)0.0 : v;
+            };
+            total = total + pairwise_row<I>(nx, val);
+          } else {
+            auto val = [&](int si) -> double {
+              const I v = brow[lds_pos(kb + si)];
+              isum += (int64_t)v;
+              iprod *= (int64_t)v;
+              nonzero += v != 0 ? 1 : 0;
+              if (!have) { imx = (int64_t)v; have = true; }
+              else if (a.agg == AGG_MAX) imx = max(imx, (int64_t)v);
+              else if (a.agg == AGG_MIN) imx = min(imx, (int64_t)v);
+              return (double)v;
+            };
+            dtotal = dtotal + pairwise_row<double>(nx, val);
+          }
         }
+      }
+      __syncthreads();  // the next group overwrites the band
+    }
+
+    const int64_t oj = oj0 + ty, oi = oi0 + tx;
+    if (ty < rows && oi < a.out_w) {
+      const int64_t didx = t * a.dst_st + oj * a.dst_sy + oi;
+      if (std::is_floating_point<I>::value) {
         double res;
         if (a.agg == AGG_MEAN) res = (double)(I)((double)total / (double)cnt);
         else if (a.agg == AGG_SUM) res = (double)total;
         else if (a.agg == AGG_PROD) res = (double)prod;
-        else if (a.agg == AGG_COUNT) res = 0.0;
         else res = (double)mx;
         if (a.agg == AGG_COUNT) store_any(a.dst, didx, a.dst_dtype, 0.0, nonzero, true);
         else store_any(a.dst, didx, a.dst_dtype, res, 0, false);
       } else {
-        // integer reducers: mean via float64 (np.mean) + rint; sum/prod in int64
-        double total = 0.0;
-        int64_t isum = 0, iprod = 1, nonzero = 0, mx = 0;
-        bool have = false;
-        for (int sj = 0; sj < ny; ++sj) {
-          const AxisTab ey = a.ytab[oj * a.dy + sj];
-          auto val = [&](int si) -> double {
-            const I v = subsample<T, I, ORDER, RECOVER>(p, ey, a.xtab[oi * a.dx + si], has_t1,
-                                                        a.cval);
-            isum += (int64_t)v;
-            iprod *= (int64_t)v;
-            nonzero += v != 0 ? 1 : 0;
-            if (!have) { mx = (int64_t)v; have = true; }
-            else if (a.agg == AGG_MAX) mx = max(mx, (int64_t)v);
-            else if (a.agg == AGG_MIN) mx = min(mx, (int64_t)v);
-            return (double)v;
-          };
-          total = total + pairwise_row<double>(nx, val);
-        }
         if (a.agg == AGG_MEAN) {
-          const double m = rint(total / (double)(ny * nx));
+          const double m = rint(dtotal / (double)(ny * nx));
           store_any(a.dst, didx, a.dst_dtype, 0.0, (int64_t)Conv<T>::from_f64(m), true);
         } else if (a.agg == AGG_SUM) {
           store_any(a.dst, didx, a.dst_dtype, 0.0, isum, true);
@@ -403,12 +506,19 @@ affine_kernel(AffineArgs a) {
         } else if (a.agg == AGG_COUNT) {
           store_any(a.dst, didx, a.dst_dtype, 0.0, nonzero, true);
         } else {
-          store_any(a.dst, didx, a.dst_dtype, 0.0, mx, true);
+          store_any(a.dst, didx, a.dst_dtype, 0.0, imx, true);
         }
       }
     }
-    __syncthreads();  // the next tile overwrites the patch
   }
+}
+
+constexpr int kReduceLdsBudget = 32 * 1024;   // intermediate band
+
+// LDS bytes of one intermediate row of a reduce tile
+inline int64_t reduce_row_bytes(int64_t dx, int64_t isize) {
+  const int64_t band_w = kTileW * dx;
+  return (band_w + (band_w - 1) / 32) * isize;
 }
 
 template <typename T, typename I, int ORDER, bool RECOVER>
@@ -421,10 +531,41 @@ int launch(const AffineArgs& a, const AxisChunks& ay, const AxisChunks& ax, Axis
   AffineArgs args = a;
   args.ytab = ytab;
   args.xtab = xtab;
-  const int64_t ntiles = ((a.out_w + kTileW - 1) / kTileW) * ((a.out_h + kTileH - 1) / kTileH) * a.nt;
-  const int nb = grid_blocks(ntiles, 1, 256 * 4);
-  hipLaunchKernelGGL((affine_kernel<T, I, ORDER, RECOVER>), dim3(nb), dim3(kThreads), kLdsBytes,
-                     st, args);
+  const bool direct = a.agg == AGG_NONE || a.agg == AGG_FIRST || a.agg == AGG_LAST ||
+                      a.agg == AGG_CENTER;
+  if (direct) {
+    const int64_t ntiles =
+        ((a.out_w + kTileW - 1) / kTileW) * ((a.out_h + kTileH - 1) / kTileH) * a.nt;
+    const int nb = grid_blocks(ntiles, 1, 256 * 64);
+    hipLaunchKernelGGL((affine_direct_kernel<T, I, ORDER, RECOVER>), dim3(nb), dim3(kThreads), 0,
+                       st, args, ytab, xtab);
+  } else {
+    const int64_t row_bytes = reduce_row_bytes(a.dx, sizeof(I));
+    int64_t group = kReduceLdsBudget / (kRedRows * row_bytes);
+    if (group < 1) group = 1;
+    if (group > a.dy) group = a.dy;
+    const int64_t band = group * kRedRows * row_bytes;
+    if (band > 64 * 1024) {
+      xrs_set_error("xrs_affine: coarsen factor too large for one LDS band");
+      return XRS_ERR_ARG;
+    }
+    const int64_t nty = (a.out_h + kRedRows - 1) / kRedRows;
+    const int64_t ntx = (a.out_w + kTileW - 1) / kTileW;
+    const int64_t ntiles = ntx * nty * a.nt;
+    const int nb = grid_blocks(ntiles, 1, 256 * 16);
+    // sub-sample rows whose taps are loaded together (A/B knob XRS_AFFINE_BATCH)
+    static const char* knob = std::getenv("XRS_AFFINE_BATCH");
+    const int kb = knob ? std::atoi(knob) : 2;
+    if (kb == 8)
+      hipLaunchKernelGGL((affine_reduce_kernel<T, I, ORDER, RECOVER, 8>), dim3(nb),
+                         dim3(kThreads), (size_t)band, st, args, ytab, xtab, (int)group);
+    else if (kb == 2)
+      hipLaunchKernelGGL((affine_reduce_kernel<T, I, ORDER, RECOVER, 2>), dim3(nb),
+                         dim3(kThreads), (size_t)band, st, args, ytab, xtab, (int)group);
+    else
+      hipLaunchKernelGGL((affine_reduce_kernel<T, I, ORDER, RECOVER, 4>), dim3(nb),
+                         dim3(kThreads), (size_t)band, st, args, ytab, xtab, (int)group);
+  }
   XRS_HIP_CHECK(hipGetLastError());
   return XRS_OK;
 }
