@@ -28,7 +28,8 @@ def main():
     import bench
     from xcube_resampling_amd import kernels
 
-    variants = [int(v) for v in args.variants.split(",")]
+    # an arm is "V" or "V@B": kernel variant V, B blocks per CU
+    variants = args.variants.split(",")
     _, _, plan, _, _ = bench.workload(args.size, 2048)
     dev = torch.device("cuda", 0)
     src = torch.rand((1, args.size, args.size), device=dev, dtype=torch.float32)
@@ -36,9 +37,16 @@ def main():
             for v in variants}
     out_dt = np.float32 if args.interp == "bilinear" else None
     times = {v: [] for v in variants}
+    rng = np.random.default_rng(0)
     for rnd in range(args.rounds):
-        for v in variants:
-            os.environ["XRS_REPROJECT_VARIANT"] = str(v)
+        for v in rng.permutation(variants):  # shuffled: no fixed first-in-round bias
+            v = str(v)
+            var, _, bpc = v.partition("@")
+            os.environ["XRS_REPROJECT_VARIANT"] = var
+            if bpc:
+                os.environ["XRS_REPROJECT_BLOCKS_PER_CU"] = bpc
+            else:
+                os.environ.pop("XRS_REPROJECT_BLOCKS_PER_CU", None)
             kernels.reproject(src, plan, args.interp, np.nan, out_dtype=out_dt, out=outs[v])
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()

@@ -311,7 +311,7 @@ gather_separable_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t bands_
 // No carried rows: every target row loads its two source rows (the ceil/floor
 // overlap of neighbouring rows is served by L1/L2), but the loads of kRowsB
 // rows are independent and in flight together (memory-level parallelism).
-template <typename T, typename O, int INTERP, int kRowsB>
+template <typename T, typename O, int INTERP, int kRowsB, bool NT = false>
 __global__ void __launch_bounds__(kThreads)
 gather_separable_mlp_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t bands_per_tile,
                             int64_t segs_per_tile, int64_t nwork) {
@@ -375,8 +375,127 @@ gather_separable_mlp_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t ba
               const T v11 = (okc && xc) ? v[q][3][k] : fill;
               out = Conv<O>::from_f64(interp4<T, INTERP>(v00, v01, v10, v11, dx[k], ye[q].d));
             }
-            if (lc < ncols) dst[(r + q) * a.dst_sy + lc] = out;
+            if (lc < ncols) {
+              if (NT) __builtin_nontemporal_store(out, &dst[(r + q) * a.dst_sy + lc]);
+              else dst[(r + q) * a.dst_sy + lc] = out;
+            }
           }
+        }
+      }
+    }
+  }
+}
+
+// ---- K1b'': bilinear with source-row reuse --------------------------------
+// reproject.py:315-328 computes per target pixel u0 = lerp(row floor),
+// u1 = lerp(row ceil), out = u0 + dy*(u1 - u0).  The horizontal lerp of a
+// source row only depends on (row, column), so when consecutive target rows
+// share a source row (ceil of row r == floor of row r+1, or the same floor)
+// the value is reused bit for bit instead of recomputed — one third fewer
+// float64 operations; the decisions are block-uniform (row entries are).
+// COND_LOADS additionally skips the loads of reused rows.
+template <typename T, typename O, int kRowsB, bool NT, bool COND_LOADS>
+__global__ void __launch_bounds__(kThreads)
+gather_bilinear_reuse_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t bands_per_tile,
+                             int64_t segs_per_tile, int64_t nwork) {
+  const Geometry& g = a.g;
+  const T fill = Conv<T>::from_f64(a.fill);
+  const XcdSlice sl = xcd_slice(nwork);
+  for (int64_t w = sl.first; w < sl.end; w += sl.step) {
+    WorkItem it;
+    if (!work_item(g, w, ty0, nsegs, bands_per_tile, segs_per_tile, it)) continue;
+    const AxisEntry* xt = a.xtab + it.t * g.tile_w + (it.c0 - it.tx * g.tile_w);
+    const int ncols = (int)(it.c1 - it.c0);
+    int32_t cf[kPx], cc[kPx];
+    double dx[kPx];
+#pragma unroll
+    for (int k = 0; k < kPx; ++k) {
+      const int lc = (int)threadIdx.x + k * kThreads;
+      AxisEntry e{-1, -1, 0.0};
+      if (lc < ncols) e = xt[lc];
+      cf[k] = e.f;
+      cc[k] = e.c;
+      dx[k] = e.d;
+    }
+    const AxisEntry* yt = a.ytab + it.t * g.tile_h - it.ty * g.tile_h;
+    for (int64_t sn = 0; sn < a.n; ++sn) {
+      const T* __restrict__ src = static_cast<const T*>(a.src) + sn * a.src_sn;
+      O* __restrict__ dst = static_cast<O*>(a.dst) + sn * a.dst_sn - g.row_begin * a.dst_sy + it.c0;
+      // carried: source rows of the previous target row and their lerps
+      int32_t pf = INT32_MIN, pc = INT32_MIN;
+      double ptop[kPx], pbot[kPx];
+#pragma unroll
+      for (int k = 0; k < kPx; ++k) ptop[k] = pbot[k] = 0.0;
+      for (int64_t r = it.r0; r < it.r1; r += kRowsB) {
+        AxisEntry ye[kRowsB];
+        bool need_f[kRowsB], need_c[kRowsB];
+        T v[kRowsB][4][kPx];
+        {
+          int32_t qf = pf, qc = pc;
+#pragma unroll
+          for (int q = 0; q < kRowsB; ++q) {
+            ye[q] = (r + q < it.r1) ? yt[r + q] : AxisEntry{-1, -1, 0.0};
+            // which rows' lerps can be taken from the previous target row
+            need_f[q] = !(ye[q].f == qf || ye[q].f == qc);
+            need_c[q] = !(ye[q].c == ye[q].f || ye[q].c == qc);
+            qf = ye[q].f;
+            qc = ye[q].c;
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < kRowsB; ++q) {
+          const T* rf = src + (int64_t)max(ye[q].f, 0) * a.src_sy;
+          const T* rc = src + (int64_t)max(ye[q].c, 0) * a.src_sy;
+          if (!COND_LOADS || need_f[q]) {
+#pragma unroll
+            for (int k = 0; k < kPx; ++k) {
+              v[q][0][k] = rf[max(cf[k], 0)];
+              v[q][1][k] = rf[max(cc[k], 0)];
+            }
+          }
+          if (!COND_LOADS || need_c[q]) {
+#pragma unroll
+            for (int k = 0; k < kPx; ++k) {
+              v[q][2][k] = rc[max(cf[k], 0)];
+              v[q][3][k] = rc[max(cc[k], 0)];
+            }
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < kRowsB; ++q) {
+          if (r + q >= it.r1) break;
+          const bool okf = ye[q].f >= 0, okc = ye[q].c >= 0;
+          double top[kPx], bot[kPx];
+#pragma unroll
+          for (int k = 0; k < kPx; ++k) {
+            const bool xf = cf[k] >= 0, xc = cc[k] >= 0;
+            if (need_f[q]) {
+              const T v00 = (okf && xf) ? v[q][0][k] : fill;
+              const T v01 = (okf && xc) ? v[q][1][k] : fill;
+              top[k] = Conv<T>::to_f64(v00) + dx[k] * Conv<T>::to_f64(Conv<T>::diff(v01, v00));
+            } else {
+              top[k] = ye[q].f == pf ? ptop[k] : pbot[k];
+            }
+            if (ye[q].c == ye[q].f) {
+              bot[k] = top[k];
+            } else if (need_c[q]) {
+              const T v10 = (okc && xf) ? v[q][2][k] : fill;
+              const T v11 = (okc && xc) ? v[q][3][k] : fill;
+              bot[k] = Conv<T>::to_f64(v10) + dx[k] * Conv<T>::to_f64(Conv<T>::diff(v11, v10));
+            } else {
+              bot[k] = pbot[k];
+            }
+            const O out = Conv<O>::from_f64(top[k] + ye[q].d * (bot[k] - top[k]));
+            const int lc = (int)threadIdx.x + k * kThreads;
+            if (lc < ncols) {
+              if (NT) __builtin_nontemporal_store(out, &dst[(r + q) * a.dst_sy + lc]);
+              else dst[(r + q) * a.dst_sy + lc] = out;
+            }
+            ptop[k] = top[k];
+            pbot[k] = bot[k];
+          }
+          pf = ye[q].f;
+          pc = ye[q].c;
         }
       }
     }
@@ -430,12 +549,15 @@ gather_2d_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t bands_per_til
 
 // Separable gather variant (XRS_REPROJECT_VARIANT, for A/B measurements; all
 // variants are bit-identical, only the load schedule differs):
-//   0  rows carried in registers (fewest loads, one source row in flight)
-//   1/3/2  loads of 2/3/4 target rows issued together (default 2: measured
-//      fastest on MI355X, 40960^2 bilinear 2.85 ms vs 5.1 ms for variant 0)
+//   0      rows carried in registers (fewest loads, one source row in flight)
+//   1/3/2  loads of 2/3/4 target rows issued together
+//   5/4/8  the same for 2/4/8 rows with non-temporal (streaming) output stores
+//   6/7    bilinear with source-row lerp reuse (7: also skips reused loads)
+// Default 4.  Interleaved A/B on MI355X, 40960^2 bilinear, one work item per
+// block: 4 = 2.54 ms, 2 = 2.62, 6 = 2.63 (scripts/ab_reproject.py).
 inline int variant() {
   const char* v = getenv("XRS_REPROJECT_VARIANT");
-  return v ? atoi(v) : 2;
+  return v ? atoi(v) : 4;
 }
 
 template <typename T, typename O, int INTERP>
@@ -447,7 +569,12 @@ int launch(const GatherArgs& a, int coord_mode, AxisEntry* xtab, AxisEntry* ytab
   const int64_t segs_per_tile = (g.tile_w + kSegW - 1) / kSegW;
   const int64_t nsegs = g.ntiles_x * segs_per_tile;
   const int64_t nwork = (ty1 - ty0) * bands_per_tile * nsegs;
-  const int nb = grid_blocks(nwork, 1, 256 * 8);
+  // One work item per block (measured fastest: short blocks let the dispatcher
+  // balance the CUs and keep each XCD's concurrent row set L2-sized; a
+  // persistent grid of 8 blocks/CU was 12 % slower).  A/B knob: blocks per CU.
+  const char* bpc_env = getenv("XRS_REPROJECT_BLOCKS_PER_CU");
+  const int bpc = bpc_env ? atoi(bpc_env) : 0;
+  const int nb = grid_blocks(nwork, 1, bpc > 0 ? 256 * bpc : (1 << 24));
   GatherArgs args = a;
   if (coord_mode == 0) {
     const int64_t ntab = g.ntiles_x * g.ntiles_y * (g.tile_w + g.tile_h);
@@ -467,6 +594,26 @@ int launch(const GatherArgs& a, int coord_mode, AxisEntry* xtab, AxisEntry* ytab
     else if (v == 3)
       hipLaunchKernelGGL((gather_separable_mlp_kernel<T, O, INTERP, 3>), dim3(nb), dim3(kThreads),
                          0, stream, args, ty0, nsegs, bands_per_tile, segs_per_tile, nwork);
+    else if (v == 4)
+      hipLaunchKernelGGL((gather_separable_mlp_kernel<T, O, INTERP, 4, true>), dim3(nb),
+                         dim3(kThreads), 0, stream, args, ty0, nsegs, bands_per_tile,
+                         segs_per_tile, nwork);
+    else if (v == 5)
+      hipLaunchKernelGGL((gather_separable_mlp_kernel<T, O, INTERP, 2, true>), dim3(nb),
+                         dim3(kThreads), 0, stream, args, ty0, nsegs, bands_per_tile,
+                         segs_per_tile, nwork);
+    else if (v == 8)
+      hipLaunchKernelGGL((gather_separable_mlp_kernel<T, O, INTERP, 8, true>), dim3(nb),
+                         dim3(kThreads), 0, stream, args, ty0, nsegs, bands_per_tile,
+                         segs_per_tile, nwork);
+    else if (v == 6 && INTERP == XRS_INTERP_BILINEAR)
+      hipLaunchKernelGGL((gather_bilinear_reuse_kernel<T, O, 4, true, false>), dim3(nb),
+                         dim3(kThreads), 0, stream, args, ty0, nsegs, bands_per_tile,
+                         segs_per_tile, nwork);
+    else if (v == 7 && INTERP == XRS_INTERP_BILINEAR)
+      hipLaunchKernelGGL((gather_bilinear_reuse_kernel<T, O, 4, true, true>), dim3(nb),
+                         dim3(kThreads), 0, stream, args, ty0, nsegs, bands_per_tile,
+                         segs_per_tile, nwork);
     else
       hipLaunchKernelGGL((gather_separable_kernel<T, O, INTERP>), dim3(nb), dim3(kThreads), 0,
                          stream, args, ty0, nsegs, bands_per_tile, segs_per_tile, nwork);
