@@ -252,7 +252,7 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
-                "kernel": "gather_separable_mlp_kernel<float,float,1,4,true> (+ axis_tables_kernel<1>, <0.6%)",
+                "kernel": "gather_separable_mlp_kernel<float,float,1,8,true,2> (+ axis_tables_kernel<1>, <0.6%)",
                 "kernel_ms": round(kernel_ms, 4),
                 "algorithmic_bytes": int(alg_bytes),
             },

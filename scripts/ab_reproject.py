@@ -28,7 +28,7 @@ def main():
     import bench
     from xcube_resampling_amd import kernels
 
-    # an arm is "V" or "V@B": kernel variant V, B blocks per CU
+    # an arm is "V", "V@B" or "V@B/R": kernel variant V, B blocks per CU, R rows per item
     variants = args.variants.split(",")
     _, _, plan, _, _ = bench.workload(args.size, 2048)
     dev = torch.device("cuda", 0)
@@ -41,12 +41,14 @@ def main():
     for rnd in range(args.rounds):
         for v in rng.permutation(variants):  # shuffled: no fixed first-in-round bias
             v = str(v)
-            var, _, bpc = v.partition("@")
+            var, _, rest = v.partition("@")
+            bpc, _, band = rest.partition("/")
             os.environ["XRS_REPROJECT_VARIANT"] = var
-            if bpc:
-                os.environ["XRS_REPROJECT_BLOCKS_PER_CU"] = bpc
-            else:
-                os.environ.pop("XRS_REPROJECT_BLOCKS_PER_CU", None)
+            for name, val in (("XRS_REPROJECT_BLOCKS_PER_CU", bpc), ("XRS_REPROJECT_BAND", band)):
+                if val and val != "0":
+                    os.environ[name] = val
+                else:
+                    os.environ.pop(name, None)
             kernels.reproject(src, plan, args.interp, np.nan, out_dtype=out_dt, out=outs[v])
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()

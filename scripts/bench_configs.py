@@ -123,7 +123,7 @@ def config2(args):
     cpu = bench.cpu_baseline(plan, src_gm, lon, lat, tgm, args.cpu_seconds)
     _line(2, "reproject bilinear 8192x8192 f32 EPSG:4326->EPSG:3857, 2048^2 tiles, f64 out "
              "(the reference's bilinear dtype)", size * size, ms, wall,
-          8 * size * size + 4 * s_read, "gather_separable_mlp_kernel<float,double,1,4>", cpu)
+          8 * size * size + 4 * s_read, "gather_separable_mlp_kernel<float,double,1,8,true,2>", cpu)
 
 
 # ------------------------------------------------------------------ config 3

@@ -74,7 +74,7 @@ def reduce(d):
     bench_read = fetch[1] * 1024 * k_fetch
     bench_write = write[1] * 1024 * k_write
     res = {
-        "size": SIZE, "out_dtype": "f32", "kernel": "gather_separable_mlp_kernel<float,float,1,4,true> (non-temporal stores, one work item per block)",
+        "size": SIZE, "out_dtype": "f32", "kernel": "gather_separable_mlp_kernel<float,float,1,8,true,2> (non-temporal stores, one work item per block)",
         "hbm_bytes_per_launch": int(bench_read + bench_write),
         "read_bytes": int(bench_read), "write_bytes": int(bench_write),
         "raw_fetch_kib": fetch, "raw_write_kib": write,

@@ -38,6 +38,33 @@ def test_kernel_matches_reference_bitwise(case, interp):
     assert_bitwise_equal(out.cpu().numpy(), g[f"out_{interp}"], f"{case}/{interp}")
 
 
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13])
+def test_every_gather_variant_is_bit_identical(variant, monkeypatch):
+    """The A/B schedules of K1 (XRS_REPROJECT_VARIANT) differ only in load
+    order / work shape: all reproduce the reference bit for bit, incl. a small
+    band height (items that split tiles) and a single block per CU (grid loop)."""
+    import torch
+
+    import xcube_resampling_amd as xrs
+    from xcube_resampling_amd import kernels
+
+    monkeypatch.setenv("XRS_REPROJECT_VARIANT", str(variant))
+    for case in ("f32", "i16"):
+        g = load_golden(f"reproject_{case}.npz")
+        ds, tgm = reproject_golden_inputs(g)
+        sgm = xrs.GridMapping.from_dataset(ds)
+        plan = xrs.plan_reproject(sgm, tgm, xrs.Transformer.from_crs(tgm.crs, sgm.crs,
+                                                                      always_xy=True))
+        src = torch.from_numpy(g["data"]).cuda()
+        for interp in ("nearest", "bilinear", "triangular"):
+            for band, bpc in (("", ""), ("5", "1")):
+                monkeypatch.setenv("XRS_REPROJECT_BAND", band or "0")
+                monkeypatch.setenv("XRS_REPROJECT_BLOCKS_PER_CU", bpc or "0")
+                out = kernels.reproject(src, plan, interp, g["fill"].item())
+                assert_bitwise_equal(out.cpu().numpy(), g[f"out_{interp}"],
+                                     f"v{variant} {case}/{interp} band={band} bpc={bpc}")
+
+
 @pytest.mark.parametrize("case", NO_DOWNSCALE)
 @pytest.mark.parametrize("interp", ["nearest", "bilinear", "triangular"])
 def test_reproject_dataset_matches_reference_bitwise(case, interp):

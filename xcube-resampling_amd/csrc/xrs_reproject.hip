@@ -62,6 +62,8 @@ struct Geometry {
   int64_t win_h, win_w;
   double x_res, neg_y_res;
   int32_t* err_flags;
+  int64_t band;   // target rows per work item of the gathers
+  int64_t segw;   // target columns per work item (kThreads x columns per thread)
 };
 
 // numpy fancy index on a window axis of length `win` with an int16 index:
@@ -192,12 +194,12 @@ __device__ inline bool work_item(const Geometry& g, int64_t w, int64_t ty0, int6
   it.ty = ty0 + tyi;
   const int64_t bi = b - tyi * bands_per_tile;
   const int64_t tr0 = it.ty * g.tile_h;
-  it.r0 = max(g.row_begin, tr0 + bi * kBand);
-  it.r1 = min(min(g.row_end, tr0 + g.tile_h), tr0 + bi * kBand + kBand);
+  it.r0 = max(g.row_begin, tr0 + bi * g.band);
+  it.r1 = min(min(g.row_end, tr0 + g.tile_h), tr0 + bi * g.band + g.band);
   it.tx = s / segs_per_tile;
   const int64_t si = s - it.tx * segs_per_tile;
-  it.c0 = it.tx * g.tile_w + si * kSegW;
-  it.c1 = min(min(g.dst_w, it.tx * g.tile_w + g.tile_w), it.c0 + kSegW);
+  it.c0 = it.tx * g.tile_w + si * g.segw;
+  it.c1 = min(min(g.dst_w, it.tx * g.tile_w + g.tile_w), it.c0 + g.segw);
   it.t = it.ty * g.ntiles_x + it.tx;
   return it.r0 < it.r1 && it.c0 < it.c1;
 }
@@ -311,7 +313,7 @@ gather_separable_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t bands_
 // No carried rows: every target row loads its two source rows (the ceil/floor
 // overlap of neighbouring rows is served by L1/L2), but the loads of kRowsB
 // rows are independent and in flight together (memory-level parallelism).
-template <typename T, typename O, int INTERP, int kRowsB, bool NT = false>
+template <typename T, typename O, int INTERP, int kRowsB, bool NT = false, int PX = kPx>
 __global__ void __launch_bounds__(kThreads)
 gather_separable_mlp_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t bands_per_tile,
                             int64_t segs_per_tile, int64_t nwork) {
@@ -323,10 +325,10 @@ gather_separable_mlp_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t ba
     if (!work_item(g, w, ty0, nsegs, bands_per_tile, segs_per_tile, it)) continue;
     const AxisEntry* xt = a.xtab + it.t * g.tile_w + (it.c0 - it.tx * g.tile_w);
     const int ncols = (int)(it.c1 - it.c0);
-    int32_t cf[kPx], cc[kPx];
-    double dx[kPx];
+    int32_t cf[PX], cc[PX];
+    double dx[PX];
 #pragma unroll
-    for (int k = 0; k < kPx; ++k) {
+    for (int k = 0; k < PX; ++k) {
       const int lc = (int)threadIdx.x + k * kThreads;
       AxisEntry e{-1, -1, 0.0};
       if (lc < ncols) e = xt[lc];
@@ -340,14 +342,14 @@ gather_separable_mlp_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t ba
       O* __restrict__ dst = static_cast<O*>(a.dst) + sn * a.dst_sn - g.row_begin * a.dst_sy + it.c0;
       for (int64_t r = it.r0; r < it.r1; r += kRowsB) {
         AxisEntry ye[kRowsB];
-        T v[kRowsB][4][kPx];
+        T v[kRowsB][4][PX];
 #pragma unroll
         for (int q = 0; q < kRowsB; ++q) {
           ye[q] = (r + q < it.r1) ? yt[r + q] : AxisEntry{-1, -1, 0.0};
           const T* rf = src + (int64_t)max(ye[q].f, 0) * a.src_sy;
           const T* rc = src + (int64_t)max(ye[q].c, 0) * a.src_sy;
 #pragma unroll
-          for (int k = 0; k < kPx; ++k) {
+          for (int k = 0; k < PX; ++k) {
             const int32_t f = max(cf[k], 0), c = max(cc[k], 0);
             v[q][0][k] = rf[f];
             if (INTERP != XRS_INTERP_NEAREST) {
@@ -362,7 +364,7 @@ gather_separable_mlp_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t ba
           if (r + q >= it.r1) break;
           const bool okf = ye[q].f >= 0, okc = ye[q].c >= 0;
 #pragma unroll
-          for (int k = 0; k < kPx; ++k) {
+          for (int k = 0; k < PX; ++k) {
             const int lc = (int)threadIdx.x + k * kThreads;
             const bool xf = cf[k] >= 0, xc = cc[k] >= 0;
             const T v00 = (okf && xf) ? v[q][0][k] : fill;
@@ -553,11 +555,14 @@ gather_2d_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t bands_per_til
 //   1/3/2  loads of 2/3/4 target rows issued together
 //   5/4/8  the same for 2/4/8 rows with non-temporal (streaming) output stores
 //   6/7    bilinear with source-row lerp reuse (7: also skips reused loads)
-// Default 4.  Interleaved A/B on MI355X, 40960^2 bilinear, one work item per
-// block: 4 = 2.54 ms, 2 = 2.62, 6 = 2.63 (scripts/ab_reproject.py).
+//   9/10/11  as 4 with 2/8/1 columns per thread (512/2048/256-column items)
+//   12/13  8/16 rows in flight, 2 columns per thread, non-temporal stores
+// Default 12.  Interleaved A/B on one MI355X, 40960^2 bilinear, one work item
+// per block: 12 = 2.51 ms, 9 = 2.57, 4 = 2.76, 11 = 2.96, 13 = 3.69
+// (scripts/ab_reproject.py; absolute times vary ~10 % between boxes).
 inline int variant() {
   const char* v = getenv("XRS_REPROJECT_VARIANT");
-  return v ? atoi(v) : 4;
+  return v ? atoi(v) : 12;
 }
 
 template <typename T, typename O, int INTERP>
@@ -565,8 +570,13 @@ int launch(const GatherArgs& a, int coord_mode, AxisEntry* xtab, AxisEntry* ytab
            hipStream_t stream) {
   const Geometry& g = a.g;
   const int64_t ty0 = g.row_begin / g.tile_h, ty1 = (g.row_end - 1) / g.tile_h + 1;
-  const int64_t bands_per_tile = (g.tile_h + kBand - 1) / kBand;
-  const int64_t segs_per_tile = (g.tile_w + kSegW - 1) / kSegW;
+  const char* band_env = getenv("XRS_REPROJECT_BAND");  // A/B knob (target rows per item)
+  GatherArgs args = a;
+  args.g.band = band_env && atoi(band_env) > 0 ? atoi(band_env) : kBand;
+  const int64_t bands_per_tile = (g.tile_h + args.g.band - 1) / args.g.band;
+  const int v = variant();
+  args.g.segw = kThreads * (v == 9 || v == 12 || v == 13 ? 2 : v == 10 ? 8 : v == 11 ? 1 : kPx);
+  const int64_t segs_per_tile = (g.tile_w + args.g.segw - 1) / args.g.segw;
   const int64_t nsegs = g.ntiles_x * segs_per_tile;
   const int64_t nwork = (ty1 - ty0) * bands_per_tile * nsegs;
   // One work item per block (measured fastest: short blocks let the dispatcher
@@ -575,7 +585,6 @@ int launch(const GatherArgs& a, int coord_mode, AxisEntry* xtab, AxisEntry* ytab
   const char* bpc_env = getenv("XRS_REPROJECT_BLOCKS_PER_CU");
   const int bpc = bpc_env ? atoi(bpc_env) : 0;
   const int nb = grid_blocks(nwork, 1, bpc > 0 ? 256 * bpc : (1 << 24));
-  GatherArgs args = a;
   if (coord_mode == 0) {
     const int64_t ntab = g.ntiles_x * g.ntiles_y * (g.tile_w + g.tile_h);
     const int nbt = grid_blocks(ntab, kThreads, 256 * 8);
@@ -584,7 +593,6 @@ int launch(const GatherArgs& a, int coord_mode, AxisEntry* xtab, AxisEntry* ytab
     XRS_HIP_CHECK(hipGetLastError());
     args.xtab = xtab;
     args.ytab = ytab;
-    const int v = variant();
     if (v == 1)
       hipLaunchKernelGGL((gather_separable_mlp_kernel<T, O, INTERP, 2>), dim3(nb), dim3(kThreads),
                          0, stream, args, ty0, nsegs, bands_per_tile, segs_per_tile, nwork);
@@ -604,6 +612,26 @@ int launch(const GatherArgs& a, int coord_mode, AxisEntry* xtab, AxisEntry* ytab
                          segs_per_tile, nwork);
     else if (v == 8)
       hipLaunchKernelGGL((gather_separable_mlp_kernel<T, O, INTERP, 8, true>), dim3(nb),
+                         dim3(kThreads), 0, stream, args, ty0, nsegs, bands_per_tile,
+                         segs_per_tile, nwork);
+    else if (v == 9)
+      hipLaunchKernelGGL((gather_separable_mlp_kernel<T, O, INTERP, 4, true, 2>), dim3(nb),
+                         dim3(kThreads), 0, stream, args, ty0, nsegs, bands_per_tile,
+                         segs_per_tile, nwork);
+    else if (v == 10)
+      hipLaunchKernelGGL((gather_separable_mlp_kernel<T, O, INTERP, 4, true, 8>), dim3(nb),
+                         dim3(kThreads), 0, stream, args, ty0, nsegs, bands_per_tile,
+                         segs_per_tile, nwork);
+    else if (v == 11)
+      hipLaunchKernelGGL((gather_separable_mlp_kernel<T, O, INTERP, 4, true, 1>), dim3(nb),
+                         dim3(kThreads), 0, stream, args, ty0, nsegs, bands_per_tile,
+                         segs_per_tile, nwork);
+    else if (v == 12)
+      hipLaunchKernelGGL((gather_separable_mlp_kernel<T, O, INTERP, 8, true, 2>), dim3(nb),
+                         dim3(kThreads), 0, stream, args, ty0, nsegs, bands_per_tile,
+                         segs_per_tile, nwork);
+    else if (v == 13)
+      hipLaunchKernelGGL((gather_separable_mlp_kernel<T, O, INTERP, 16, true, 2>), dim3(nb),
                          dim3(kThreads), 0, stream, args, ty0, nsegs, bands_per_tile,
                          segs_per_tile, nwork);
     else if (v == 6 && INTERP == XRS_INTERP_BILINEAR)
@@ -684,7 +712,7 @@ extern "C" int xrs_reproject(const void* src, int src_dtype, int64_t n, int64_t 
   g.ntiles_y = (dst_h + tile_h - 1) / tile_h;
   g.src_x = src_x; g.src_y = src_y; g.tile_x0 = tile_x0; g.tile_y0 = tile_y0;
   g.tile_win = tile_win; g.win_h = win_h; g.win_w = win_w;
-  g.x_res = x_res; g.neg_y_res = -y_res; g.err_flags = err_flags;
+  g.x_res = x_res; g.neg_y_res = -y_res; g.err_flags = err_flags; g.band = kBand; g.segw = kSegW;
   a.src = src; a.n = n; a.src_sn = src_sn; a.src_sy = src_sy;
   a.dst = dst; a.dst_sn = dst_sn; a.dst_sy = dst_sy; a.fill = fill;
   a.xtab = a.ytab = nullptr;
