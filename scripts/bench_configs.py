@@ -201,7 +201,7 @@ def config4(args):
     src = torch.from_numpy(var).cuda()
     xy = (dlon, dlat)
 
-    tiles, ntx, bb, _ = R.rectify_tiles(sgm, tgm)
+    tiles, ntx, bb, _ = R.rectify_tiles(sgm, tgm, xy=xy)
     dst_y_scale = -tgm.y_res
 
     def k5():
@@ -218,7 +218,7 @@ def config4(args):
         lines[interp] = k6_ms
 
     def pipeline(interp):
-        t, n_x, _, _ = R.rectify_tiles(sgm, tgm)
+        t, n_x, _, _ = R.rectify_tiles(sgm, tgm, xy=xy)
         ij_ = kernels.rectify_ij(xy[0], xy[1], t, n_x, tgm.height, tgm.width, tgm.x_res,
                                  dst_y_scale, 1e-3)
         return kernels.rectify_var(ij_, src, interp, float("nan"))
@@ -246,7 +246,7 @@ def config4(args):
         cpu_v, px, dt = _cpu_loop(cpu_once, args.cpu_seconds, 0)
         _line(4, f"rectify {interp}: 4000x4800 jittered swath (f64 lon/lat, f32 var) -> "
                  f"{tgm.width}x{tgm.height} EPSG:4326 res 0.0027, 512^2 tiles "
-                 "(K4 bbox + host tiling + K5 + K6, end to end)",
+                 "(K4 bbox + host tiling + K5 + K6, end to end, coordinates resident in HBM)",
               npx, ms, wall, 16 * S + 4 * S + 4 * npx,
               f"K5 rectify_claim+resolve {k5_ms:.3f} ms, K6 {lines[interp]:.3f} ms",
               dict(value=round(cpu_v, 2), unit="Mpixels/s", cores=cores, kind="port",

@@ -24,6 +24,7 @@
 //                every index, fraction and clamp unchanged.
 
 #include <cmath>
+#include <cstdlib>
 
 #include "xrs_common.hpp"
 
@@ -59,8 +60,9 @@ struct BBoxArgs {
 };
 
 // Next candidate box > `after` that contains (x, y), or INT32_MAX.
-__device__ inline int32_t next_box(const BBoxArgs& a, double x, double y, int32_t tx0, int32_t tx1,
-                                   int32_t ty0, int32_t ty1, int32_t after) {
+__device__ inline int32_t next_box(const BBoxArgs& a, const double* bx, double x, double y,
+                                   int32_t tx0, int32_t tx1, int32_t ty0, int32_t ty1,
+                                   int32_t after) {
   if (a.ntx > 0) {  // grid: candidates = rectangle [ty0,ty1] x [tx0,tx1], row-major
     if (tx0 > tx1 || ty0 > ty1) return INT32_MAX;
     int32_t ty = ty0, tx = tx0;
@@ -73,21 +75,46 @@ __device__ inline int32_t next_box(const BBoxArgs& a, double x, double y, int32_
     return ty <= ty1 ? ty * (int32_t)a.ntx + tx : INT32_MAX;
   }
   for (int32_t k = after + 1; k < (int32_t)a.nboxes; ++k) {
-    const double* b = a.bx + 4 * k;
+    const double* b = bx + 4 * k;
     if (b[0] <= x && x <= b[2] && b[1] <= y && y <= b[3]) return k;
   }
   return INT32_MAX;
 }
 
+// Each block owns one contiguous run of source pixels (spatially coherent:
+// few boxes per block).  SHARED: the box geometry and the per-box accumulators
+// live in LDS — the wave merges go to LDS atomics and each block flushes one
+// set of global atomics per box it touched (thousands of waves hammering the
+// same few hundred global words serialised at the L2 atomic units).
+template <bool SHARED>
 __global__ void __launch_bounds__(kThreads)
-ij_bboxes_kernel(BBoxArgs a) {
+ij_bboxes_kernel(BBoxArgs a, int64_t chunk) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int64_t nbx = a.ntx > 0 ? 2 * a.ntx : 4 * a.nboxes;   // doubles of bx
+  const int64_t nby = a.ntx > 0 ? 2 * a.nty : 0;
+  double* sbx = reinterpret_cast<double*>(smem);
+  double* sby = sbx + nbx;
+  int32_t* sacc = reinterpret_cast<int32_t*>(sby + nby);
+  const double* bx = a.bx;
+  const double* by = a.by;
+  int32_t* acc = a.acc;
+  if (SHARED) {
+    for (int64_t i = threadIdx.x; i < nbx; i += kThreads) sbx[i] = a.bx[i];
+    for (int64_t i = threadIdx.x; i < nby; i += kThreads) sby[i] = a.by[i];
+    for (int64_t i = threadIdx.x; i < 4 * a.nboxes; i += kThreads)
+      sacc[i] = (i & 3) < 2 ? INT32_MAX : -1;
+    __syncthreads();
+    bx = sbx;
+    by = sby;
+    acc = sacc;
+  }
   const int64_t n = a.h * a.w;
-  const int64_t stride = (int64_t)gridDim.x * kThreads;
+  const int64_t p0 = (int64_t)blockIdx.x * chunk, p1 = min(n, p0 + chunk);
   // every lane of a wave iterates the same number of times (wave-uniform trip
   // count), so the wave-wide shuffles below always see all 64 lanes
-  for (int64_t base = (int64_t)blockIdx.x * kThreads; base < n; base += stride) {
+  for (int64_t base = p0; base < p1; base += kThreads) {
     const int64_t idx = base + threadIdx.x;
-    const bool valid = idx < n;
+    const bool valid = idx < p1;
     double x = NAN, y = NAN;
     int32_t i0 = 0, j0 = 0;
     if (valid) {
@@ -99,11 +126,11 @@ ij_bboxes_kernel(BBoxArgs a) {
     int32_t tx0 = 1, tx1 = 0, ty0 = 1, ty1 = 0;
     if (valid && a.ntx > 0) {  // x_min <= x <= x_max, y_min <= y <= y_max (bboxes.py:60-69)
       for (int32_t t = 0; t < (int32_t)a.ntx; ++t)
-        if (a.bx[2 * t] <= x && x <= a.bx[2 * t + 1]) { if (tx0 > tx1) tx0 = t; tx1 = t; }
+        if (bx[2 * t] <= x && x <= bx[2 * t + 1]) { if (tx0 > tx1) tx0 = t; tx1 = t; }
       for (int32_t t = 0; t < (int32_t)a.nty; ++t)
-        if (a.by[2 * t] <= y && y <= a.by[2 * t + 1]) { if (ty0 > ty1) ty0 = t; ty1 = t; }
+        if (by[2 * t] <= y && y <= by[2 * t + 1]) { if (ty0 > ty1) ty0 = t; ty1 = t; }
     }
-    int32_t cur = valid ? next_box(a, x, y, tx0, tx1, ty0, ty1, -1) : INT32_MAX;
+    int32_t cur = valid ? next_box(a, bx, x, y, tx0, tx1, ty0, ty1, -1) : INT32_MAX;
     while (true) {
       const int32_t k = wave_min(cur);  // next box any lane of the wave contributes to
       if (k == INT32_MAX) break;
@@ -113,12 +140,22 @@ ij_bboxes_kernel(BBoxArgs a) {
       const int32_t imax = wave_max(mine ? i0 : -1);
       const int32_t jmax = wave_max(mine ? j0 : -1);
       if ((threadIdx.x & 63) == 0) {
-        atomicMin(&a.acc[4 * k + 0], imin);
-        atomicMin(&a.acc[4 * k + 1], jmin);
-        atomicMax(&a.acc[4 * k + 2], imax);
-        atomicMax(&a.acc[4 * k + 3], jmax);
+        atomicMin(&acc[4 * k + 0], imin);
+        atomicMin(&acc[4 * k + 1], jmin);
+        atomicMax(&acc[4 * k + 2], imax);
+        atomicMax(&acc[4 * k + 3], jmax);
       }
-      if (mine) cur = next_box(a, x, y, tx0, tx1, ty0, ty1, k);
+      if (mine) cur = next_box(a, bx, x, y, tx0, tx1, ty0, ty1, k);
+    }
+  }
+  if (SHARED) {
+    __syncthreads();
+    for (int64_t k = threadIdx.x; k < a.nboxes; k += kThreads) {
+      if (sacc[4 * k + 2] < 0) continue;  // box not touched by this block
+      atomicMin(&a.acc[4 * k + 0], sacc[4 * k + 0]);
+      atomicMin(&a.acc[4 * k + 1], sacc[4 * k + 1]);
+      atomicMax(&a.acc[4 * k + 2], sacc[4 * k + 2]);
+      atomicMax(&a.acc[4 * k + 3], sacc[4 * k + 3]);
     }
   }
 }
@@ -211,6 +248,7 @@ __device__ inline void quad_dets(const RectArgs& a, int64_t qj, int64_t qi, doub
 }
 
 // ---- K5a: claim target pixels with the raster-order key of hitting quads -------
+template <bool PREREAD>
 __global__ void __launch_bounds__(kThreads)
 rectify_claim_kernel(RectArgs a) {
   for (int64_t c = blockIdx.x; c < a.nchunks; c += gridDim.x) {
@@ -242,7 +280,7 @@ rectify_claim_kernel(RectArgs a) {
       const double dy = ti.y_off + ((double)dj + 0.5) * a.y_scale;
       uint32_t* krow = a.keys + (int64_t)(ti.r0 + dj) * a.dst_w + ti.c0;
       for (int64_t di = imin; di <= imax; ++di) {
-        if (krow[di] <= key) continue;  // already claimed by an earlier quad
+        if (PREREAD && krow[di] <= key) continue;  // already claimed by an earlier quad
         const double dx = ti.x_off + ((double)di + 0.5) * a.x_scale;
         double cu, cv;
         if (quad_hit(a, qj, qi, dx, dy, det_a, det_b, cu, cv)) atomicMin(&krow[di], key);
@@ -356,7 +394,13 @@ extern "C" int xrs_ij_bboxes(const double* x, const double* y, int64_t h, int64_
   BBoxArgs a{x, y, h, w, sy, nboxes, ntx, nty, bx, by, acc};
   hipStream_t st = static_cast<hipStream_t>(stream);
   const int nb = grid_blocks(h * w, kThreads, 256 * 8);
-  hipLaunchKernelGGL(ij_bboxes_kernel, dim3(nb), dim3(kThreads), 0, st, a);
+  const int64_t chunk = ((h * w + nb - 1) / nb + kThreads - 1) / kThreads * kThreads;
+  const int64_t lds = (ntx > 0 ? 16 * (ntx + nty) : 32 * nboxes) + 16 * nboxes;
+  if (lds <= 48 * 1024)
+    hipLaunchKernelGGL(ij_bboxes_kernel<true>, dim3(nb), dim3(kThreads), (size_t)lds, st, a,
+                       chunk);
+  else
+    hipLaunchKernelGGL(ij_bboxes_kernel<false>, dim3(nb), dim3(kThreads), 0, st, a, chunk);
   XRS_HIP_CHECK(hipGetLastError());
   return XRS_OK;
 }
@@ -382,8 +426,20 @@ extern "C" int xrs_rectify_ij(const double* x, const double* y, int64_t h, int64
   hipStream_t st = static_cast<hipStream_t>(stream);
   XRS_HIP_CHECK(hipMemsetAsync(keys, 0xFF, (size_t)(dst_h * dst_w) * sizeof(uint32_t), st));
   if (nchunks > 0) {
-    const int nb = grid_blocks(nchunks, 1, 256 * 8);
-    hipLaunchKernelGGL(rectify_claim_kernel, dim3(nb), dim3(kThreads), 0, st, a);
+    // A/B knobs: XRS_RECTIFY_PREREAD (skip quads whose pixel is already
+    // claimed by a smaller key), XRS_RECTIFY_BLOCKS_PER_CU (0 = one chunk per block)
+    const char* pr = getenv("XRS_RECTIFY_PREREAD");
+    const char* bpc = getenv("XRS_RECTIFY_BLOCKS_PER_CU");
+    // measured (config 4): no pre-read 2.04 ms vs 3.42 ms (the dependent read
+    // is latency on every tested pixel, the atomicMin is fire-and-forget);
+    // one chunk per block 1.98 vs 2.04 ms
+    const bool preread = pr ? atoi(pr) != 0 : false;
+    const int cap = bpc && atoi(bpc) > 0 ? 256 * atoi(bpc) : (1 << 24);
+    const int nb = grid_blocks(nchunks, 1, cap);
+    if (preread)
+      hipLaunchKernelGGL(rectify_claim_kernel<true>, dim3(nb), dim3(kThreads), 0, st, a);
+    else
+      hipLaunchKernelGGL(rectify_claim_kernel<false>, dim3(nb), dim3(kThreads), 0, st, a);
     XRS_HIP_CHECK(hipGetLastError());
   }
   const int nb2 = grid_blocks(dst_h * dst_w, kThreads, 256 * 8);

@@ -117,9 +117,12 @@ def _downscale_source_dataset(source_ds, source_gm: GridMapping, target_gm: Grid
     return source_ds, source_gm
 
 
-def rectify_tiles(source_gm: GridMapping, target_gm: GridMapping, uv_delta: float = UV_DELTA):
+def rectify_tiles(source_gm: GridMapping, target_gm: GridMapping, uv_delta: float = UV_DELTA,
+                  xy=None):
     """Host tiling of rectify.py:312-419: xy_border, per-tile source bboxes
-    (K4), per-tile source windows and target offsets (TILE_INFO records)."""
+    (K4), per-tile source windows and target offsets (TILE_INFO records).
+    ``xy``: the source coordinates already on the device (x, y), else they are
+    taken from ``source_gm``."""
     dst_w, dst_h = target_gm.width, target_gm.height
     tw, th = target_gm.tile_width, target_gm.tile_height
     dst_x_min, dst_y_min, dst_x_max, dst_y_max = target_gm.xy_bbox
@@ -131,8 +134,12 @@ def rectify_tiles(source_gm: GridMapping, target_gm: GridMapping, uv_delta: floa
                     min(0.5 * (dst_x_max - dst_x_min), 0.5 * (dst_y_max - dst_y_min)))
     ys = chunk_sizes(dst_h, th)
     xs = chunk_sizes(dst_w, tw)
-    src_ij_bboxes = source_gm.ij_bboxes_from_xy_bboxes(
-        target_gm.xy_bboxes, xy_border=xy_border, ij_border=1, grid=(len(xs), len(ys)))
+    if xy is None:
+        src_ij_bboxes = source_gm.ij_bboxes_from_xy_bboxes(
+            target_gm.xy_bboxes, xy_border=xy_border, ij_border=1, grid=(len(xs), len(ys)))
+    else:  # base.py:565-629 on coordinates already resident in HBM
+        src_ij_bboxes = kernels.ij_bboxes(xy[0], xy[1], target_gm.xy_bboxes, xy_border, 1,
+                                          grid=(len(xs), len(ys)))
     tiles = np.zeros(len(ys) * len(xs), dtype=kernels.TILE_INFO_DTYPE)
     r0s = np.repeat(np.concatenate([[0], np.cumsum(ys)[:-1]]), len(xs))
     c0s = np.tile(np.concatenate([[0], np.cumsum(xs)[:-1]]), len(ys))
@@ -153,9 +160,12 @@ def rectify_tiles(source_gm: GridMapping, target_gm: GridMapping, uv_delta: floa
 
 def _compute_target_source_ij(source_gm: GridMapping, target_gm: GridMapping,
                               uv_delta: float):
-    """rectify.py:312-370 -> device tensor (2, H', W') float64 (K5)."""
-    tiles, ntx, _, _ = rectify_tiles(source_gm, target_gm, uv_delta)
+    """rectify.py:312-370 -> device tensor (2, H', W') float64 (K5).  The
+    source coordinates are uploaded once and shared by K4 and K5."""
+    device = require_device()
     xy = source_gm.xy_coords.data
+    xy = (to_device(xy[0], device, np.float64), to_device(xy[1], device, np.float64))
+    tiles, ntx, _, _ = rectify_tiles(source_gm, target_gm, uv_delta, xy=xy)
     dst_y_scale = target_gm.y_res if target_gm.is_j_axis_up else -target_gm.y_res
     return kernels.rectify_ij(xy[0], xy[1], tiles, ntx, target_gm.height, target_gm.width,
                               target_gm.x_res, dst_y_scale, uv_delta)
