@@ -88,3 +88,42 @@ def reference_goldens(module: str) -> dict:
             continue
         out[k] = [(np.array(e["expected"], dtype=float), e["decimal"]) for e in v]
     return out
+
+
+def _spatial_ref(code: str):
+    return xrs.DataArray(np.array(0), (), xrs.CRS.from_string(code).to_cf())
+
+
+def dataset_5x5_regular_utm():
+    """sampledata.py:95-109 (EPSG:32632)."""
+    x = np.arange(565300.0, 565800.0, 100.0)
+    y = np.arange(5934300.0, 5933800.0, -100.0)
+    return xrs.Dataset(
+        data_vars={"band_1": xrs.DataArray(np.arange(25).reshape((5, 5)), ("y", "x"),
+                                           {"grid_mapping": "spatial_ref"})},
+        coords={"x": ("x", x), "y": ("y", y), "spatial_ref": _spatial_ref("EPSG:32632")})
+
+
+def dataset_2x5x5_regular_utm():
+    """sampledata.py:112-128 (time as int64 day numbers instead of datetime64)."""
+    ds = dataset_5x5_regular_utm()
+    band = np.repeat(np.arange(25).reshape((5, 5))[np.newaxis], 2, axis=0)
+    return xrs.Dataset(
+        data_vars={"band_1": xrs.DataArray(band, ("time", "y", "x"),
+                                           {"grid_mapping": "spatial_ref"})},
+        coords={"time": ("time", np.array([0, 1])), "x": ds["x"], "y": ds["y"],
+                "spatial_ref": _spatial_ref("EPSG:32632")})
+
+
+def dataset_large_for_reproject():
+    """sampledata.py:131-157 (EPSG:3035; eager instead of dask-chunked)."""
+    nt, nx, ny = 10, 100, 100
+    x = np.linspace(3900000, 4500000, nx)
+    y = np.linspace(2600000, 3200000, ny)
+    temp = np.arange(nt * nx * ny, dtype=np.float32).reshape(nt, nx, ny)
+    return xrs.Dataset(
+        data_vars={"temperature": xrs.DataArray(temp, ("time", "y", "x"),
+                                                {"grid_mapping": "spatial_ref"}),
+                   "onedim_data": xrs.DataArray(np.arange(nt), ("time",))},
+        coords={"time": ("time", np.arange(nt)), "x": ("x", x), "y": ("y", y),
+                "spatial_ref": _spatial_ref("EPSG:3035")})

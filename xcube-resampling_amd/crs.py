@@ -7,12 +7,15 @@ PROJ's database is available here or on the GPU box, so this module restates
 the small part of PROJ the engine needs:
 
 * a registry of the CRSs the engine supports (geographic WGS 84 in both axis
-  orders, and Web Mercator), with the attributes the reference reads
-  (``is_geographic``, ``name``, ``equals``, ``to_cf``, ``axis_info``);
+  orders, Web Mercator, the UTM zones EPSG:326xx/327xx, LAEA Europe
+  EPSG:3035, and transverse Mercator / LAEA CRSs given by CF parameters), with
+  the attributes the reference reads (``is_geographic``, ``name``, ``equals``,
+  ``to_cf``, ``axis_info``);
 * ``Transformer`` with ``transform`` and ``transform_bounds`` following PROJ's
   formulas: spherical Mercator (``webmerc``: merc_s_forward / merc_s_inverse
   with ``a = 6378137``; coordinates de-scaled by the reciprocal ``ra = 1/a``;
-  radians <-> degrees through a precomputed ``unitconvert`` factor) and PROJ's
+  radians <-> degrees through a precomputed ``unitconvert`` factor), the
+  ellipsoidal ``tmerc`` and ``laea`` of projections.py, and PROJ's
   ``proj_trans_bounds`` edge densification (21 points per edge by default).
 
 If ``pyproj`` is importable, ``CRS.from_pyproj`` accepts pyproj objects for the
@@ -50,12 +53,15 @@ class CRS:
     (gridmapping/base.py:398-404, utils.py:187-189, cfconv.py).
     """
 
-    authority: str          # "EPSG" or "OGC"
-    code: str               # "4326", "CRS84", "3857"
+    authority: str          # "EPSG", "OGC" or "CF" (defined by CF parameters)
+    code: str               # "4326", "CRS84", "3857", "32632", "3035", ...
     name: str
-    kind: str               # "geographic" | "webmerc"
+    kind: str               # "geographic" | "webmerc" | "tmerc" | "laea"
     axis_order: str         # "latlon" | "lonlat" | "en"
     cf: dict = field(default_factory=dict)
+    # projection parameters (tmerc / laea): ellipsoid name, lon_0, lat_0, k0,
+    # false easting, false northing
+    params: tuple = ()
 
     # ---- pyproj-like API ------------------------------------------------
     @property
@@ -94,8 +100,7 @@ class CRS:
         other = _as_crs(other)
         if other is None:
             return False
-        same_datum_kind = self.kind == other.kind
-        if not same_datum_kind:
+        if self.kind != other.kind or self.params != other.params:
             return False
         if ignore_axis_order:
             return True
@@ -109,7 +114,7 @@ class CRS:
         return other is not None and self.equals(other)
 
     def __hash__(self) -> int:
-        return hash((self.kind, self.axis_order))
+        return hash((self.kind, self.axis_order, self.params))
 
     def __repr__(self) -> str:
         return f"<CRS {self.srs}: {self.name}>"
@@ -122,6 +127,11 @@ class CRS:
         key = value.strip().upper().replace(" ", "")
         if key in _ALIASES:
             return _REGISTRY[_ALIASES[key]]
+        code = key[5:] if key.startswith("EPSG:") else key
+        if code.isdigit():
+            c = int(code)
+            if 32601 <= c <= 32660 or 32701 <= c <= 32760:
+                return utm_crs(c % 100, south=c > 32700)
         raise ValueError(f"unsupported CRS: {value!r}")
 
     @classmethod
@@ -151,6 +161,13 @@ class CRS:
                         return _REGISTRY["OGC:CRS84"]
                     return _REGISTRY["EPSG:4326"]
         gm_name = attrs.get("grid_mapping_name")
+        wkt = attrs.get("crs_wkt") or attrs.get("spatial_ref")
+        if isinstance(wkt, str):
+            for crs in list(_REGISTRY.values()) + list(_UTM_CACHE.values()):
+                if crs.cf.get("crs_wkt") == wkt:
+                    return crs
+        if gm_name in ("transverse_mercator", "lambert_azimuthal_equal_area"):
+            return _projected_from_cf(attrs)
         if gm_name == "latitude_longitude":
             return _REGISTRY["EPSG:4326"]
         if gm_name == "mercator" and float(attrs.get("semi_major_axis", _WGS84_A)) == _WGS84_A \
@@ -198,12 +215,90 @@ _REGISTRY: dict[str, CRS] = {
                           longitude_of_projection_origin=0.0,
                           false_easting=0.0, false_northing=0.0)),
 }
+_WKT_3035 = ('PROJCRS["ETRS89-extended / LAEA Europe",BASEGEOGCRS["ETRS89"],'
+             'CONVERSION["Europe Equal Area 2001"],ID["EPSG",3035]]')
+_GRS80_B = 6356752.314140356
+
+
+def _laea_3035_cf() -> dict:
+    return dict(crs_wkt=_WKT_3035, semi_major_axis=_WGS84_A, semi_minor_axis=_GRS80_B,
+                inverse_flattening=298.257222101, reference_ellipsoid_name="GRS 1980",
+                longitude_of_prime_meridian=0.0, prime_meridian_name="Greenwich",
+                geographic_crs_name="ETRS89",
+                horizontal_datum_name="European Terrestrial Reference System 1989 ensemble",
+                projected_crs_name="ETRS89-extended / LAEA Europe",
+                grid_mapping_name="lambert_azimuthal_equal_area",
+                latitude_of_projection_origin=52.0, longitude_of_projection_origin=10.0,
+                false_easting=4321000.0, false_northing=3210000.0)
+
+
+_REGISTRY["EPSG:3035"] = CRS("EPSG", "3035", "ETRS89-extended / LAEA Europe", "laea", "en",
+                             _laea_3035_cf(),
+                             ("GRS 1980", 10.0, 52.0, 1.0, 4321000.0, 3210000.0))
+
 _ALIASES = {
     "EPSG:4326": "EPSG:4326", "WGS84": "EPSG:4326", "4326": "EPSG:4326",
     "OGC:CRS84": "OGC:CRS84", "CRS84": "OGC:CRS84", "OGC:1.3:CRS84": "OGC:CRS84",
     "URN:OGC:DEF:CRS:OGC:1.3:CRS84": "OGC:CRS84",
     "EPSG:3857": "EPSG:3857", "3857": "EPSG:3857", "EPSG:900913": "EPSG:3857",
+    "EPSG:3035": "EPSG:3035", "3035": "EPSG:3035",
 }
+_UTM_CACHE: dict[int, CRS] = {}
+
+
+def utm_crs(zone: int, south: bool = False) -> CRS:
+    """EPSG:326zz / 327zz — WGS 84 / UTM zone zz N|S (PROJ +proj=utm)."""
+    if not 1 <= zone <= 60:
+        raise ValueError(f"invalid UTM zone {zone}")
+    code = (32700 if south else 32600) + zone
+    crs = _UTM_CACHE.get(code)
+    if crs is None:
+        name = f"WGS 84 / UTM zone {zone}{'S' if south else 'N'}"
+        lon_0 = 6.0 * zone - 183.0
+        fn = 10000000.0 if south else 0.0
+        wkt = f'PROJCRS["{name}",BASEGEOGCRS["WGS 84"],CONVERSION["UTM zone {zone}' \
+              f'{"S" if south else "N"}"],ID["EPSG",{code}]]'
+        cf = dict(crs_wkt=wkt, semi_major_axis=_WGS84_A, semi_minor_axis=6356752.314245179,
+                  inverse_flattening=_WGS84_RF, reference_ellipsoid_name="WGS 84",
+                  longitude_of_prime_meridian=0.0, prime_meridian_name="Greenwich",
+                  geographic_crs_name="WGS 84",
+                  horizontal_datum_name="World Geodetic System 1984 ensemble",
+                  projected_crs_name=name, grid_mapping_name="transverse_mercator",
+                  latitude_of_projection_origin=0.0, longitude_of_central_meridian=lon_0,
+                  false_easting=500000.0, false_northing=fn,
+                  scale_factor_at_central_meridian=0.9996)
+        crs = CRS("EPSG", str(code), name, "tmerc", "en", cf,
+                  ("WGS 84", lon_0, 0.0, 0.9996, 500000.0, fn))
+        _UTM_CACHE[code] = crs
+    return crs
+
+
+def _projected_from_cf(attrs: dict) -> CRS:
+    """A transverse Mercator / LAEA CRS from its CF grid-mapping parameters
+    (the EPSG definition when the parameters are those of a UTM zone or of
+    EPSG:3035, else a CRS defined by the parameters)."""
+    gm = attrs["grid_mapping_name"]
+    rf = float(attrs.get("inverse_flattening", _WGS84_RF))
+    ell = "GRS 1980" if abs(rf - 298.257222101) < 1e-9 else "WGS 84"
+    fe = float(attrs.get("false_easting", 0.0))
+    fn = float(attrs.get("false_northing", 0.0))
+    lat_0 = float(attrs.get("latitude_of_projection_origin", 0.0))
+    if gm == "transverse_mercator":
+        lon_0 = float(attrs.get("longitude_of_central_meridian", 0.0))
+        k0 = float(attrs.get("scale_factor_at_central_meridian", 1.0))
+        zone = (lon_0 + 183.0) / 6.0
+        if ell == "WGS 84" and k0 == 0.9996 and fe == 500000.0 and lat_0 == 0.0 \
+                and zone == int(zone) and fn in (0.0, 10000000.0):
+            return utm_crs(int(zone), south=fn != 0.0)
+        params = (ell, lon_0, lat_0, k0, fe, fn)
+        return CRS("CF", "tmerc", attrs.get("projected_crs_name", "Transverse Mercator"),
+                   "tmerc", "en", dict(attrs), params)
+    lon_0 = float(attrs.get("longitude_of_projection_origin", 0.0))
+    params = (ell, lon_0, lat_0, 1.0, fe, fn)
+    if params == _REGISTRY["EPSG:3035"].params:
+        return _REGISTRY["EPSG:3035"]
+    return CRS("CF", "laea", attrs.get("projected_crs_name", "Lambert Azimuthal Equal Area"),
+               "laea", "en", dict(attrs), params)
 
 CRS_WGS84 = _REGISTRY["EPSG:4326"]
 CRS_CRS84 = _REGISTRY["OGC:CRS84"]
@@ -261,23 +356,92 @@ def webmerc_forward(lon, lat):
     return _WGS84_A * x, _WGS84_A * y
 
 
+def _ellipsoid(name: str):
+    from .projections import GRS80, WGS84
+    return GRS80 if name == "GRS 1980" else WGS84
+
+
+def _adjlon(lam):
+    """PROJ adjlon: wrap to [-pi, pi] when outside by more than the tolerance."""
+    lam = np.asarray(lam, dtype=np.float64)
+    out = np.abs(lam) >= math.pi + 1e-12
+    if not np.any(out):
+        return lam
+    wrapped = lam + math.pi
+    wrapped = wrapped - 2 * math.pi * np.floor(wrapped / (2 * math.pi)) - math.pi
+    return np.where(out, wrapped, lam)
+
+
+_PROJ_CACHE: dict = {}
+
+
+def _projection(crs: CRS):
+    """(forward, inverse) in degrees <-> metres for a projected CRS, following
+    PROJ's pj_fwd / pj_inv around the restated projection (lam0 subtraction +
+    adjlon, unit-ellipsoid scaling by a / ra, false easting / northing)."""
+    key = (crs.kind, crs.params)
+    hit = _PROJ_CACHE.get(key)
+    if hit is not None:
+        return hit
+    if crs.kind == "webmerc":
+        hit = (webmerc_forward, webmerc_inverse)
+    else:
+        from .projections import LambertAzimuthalEqualArea, TransverseMercator
+        ell_name, lon_0, lat_0, k0, x_0, y_0 = crs.params
+        ell = _ellipsoid(ell_name)
+        lam0 = lon_0 * _DEG_TO_RAD
+        phi0 = lat_0 * _DEG_TO_RAD
+        proj = (TransverseMercator(ell, k0, phi0) if crs.kind == "tmerc"
+                else LambertAzimuthalEqualArea(ell, phi0))
+        a, ra = ell.a, 1.0 / ell.a
+
+        def forward(lon, lat, proj=proj, lam0=lam0, a=a, x_0=x_0, y_0=y_0):
+            lam = _adjlon(np.asarray(lon, dtype=np.float64) * _DEG_TO_RAD - lam0)
+            phi = np.asarray(lat, dtype=np.float64) * _DEG_TO_RAD
+            x, y = proj.forward(lam, phi)
+            return a * x + x_0, a * y + y_0
+
+        def inverse(x, y, proj=proj, lam0=lam0, ra=ra, x_0=x_0, y_0=y_0):
+            xx = (np.asarray(x, dtype=np.float64) - x_0) * ra
+            yy = (np.asarray(y, dtype=np.float64) - y_0) * ra
+            lam, phi = proj.inverse(xx, yy)
+            lam = _adjlon(lam + lam0)
+            return lam * _RAD_TO_DEG_FACTOR, phi * _RAD_TO_DEG_FACTOR
+
+        hit = (forward, inverse)
+    _PROJ_CACHE[key] = hit
+    return hit
+
+
 class Transformer:
-    """Subset of ``pyproj.Transformer`` used by the reference."""
+    """Subset of ``pyproj.Transformer`` used by the reference (always_xy).
+
+    Pipelines are source -> geographic -> target; geographic CRSs on WGS 84 and
+    ETRS89 are related by PROJ's null (ballpark) datum transformation."""
 
     def __init__(self, crs_from: CRS, crs_to: CRS):
         self.source_crs = crs_from
         self.target_crs = crs_to
-        a, b = crs_from.kind, crs_to.kind
-        if a == b:
+        same = crs_from.kind == crs_to.kind and crs_from.params == crs_to.params
+        if same:
             self._fn = None
-        elif a == "webmerc" and b == "geographic":
-            self._fn = webmerc_inverse
-        elif a == "geographic" and b == "webmerc":
-            self._fn = webmerc_forward
-        else:
-            raise NotImplementedError(
-                f"transformation {crs_from.srs} -> {crs_to.srs} is not supported"
-            )
+            self._separable = True
+            return
+        steps = []
+        if not crs_from.is_geographic:
+            steps.append(_projection(crs_from)[1])
+        if not crs_to.is_geographic:
+            steps.append(_projection(crs_to)[0])
+
+        def fn(xx, yy, steps=tuple(steps)):
+            for step in steps:
+                xx, yy = step(xx, yy)
+            return xx, yy
+
+        self._fn = fn
+        # x' depends only on x and y' only on y: geographic <-> web Mercator
+        kinds = {crs_from.kind, crs_to.kind}
+        self._separable = kinds <= {"geographic", "webmerc"}
 
     @classmethod
     def from_crs(cls, crs_from, crs_to, always_xy: bool = False) -> "Transformer":
@@ -291,8 +455,9 @@ class Transformer:
 
     @property
     def is_separable(self) -> bool:
-        """x' depends only on x and y' only on y (true for every supported pair)."""
-        return True
+        """x' depends only on x and y' only on y (identity, geographic <-> web
+        Mercator); other pairs need 2-D coordinate tables."""
+        return self._separable
 
     def transform(self, xx, yy):
         xx = np.asarray(xx, dtype=np.float64)

@@ -201,21 +201,26 @@ struct RectArgs {
   double* ij;                  // (2, dst_h, dst_w) output
 };
 
-// Test triangle A then B of quad (qj, qi) (global source indices) for the
-// target pixel centre (dx, dy) (rectify.py:556-573).  Returns 0 (no hit), 1
-// (triangle A: src = p0 + clamp(u, v)) or 2 (triangle B: src = p3 - clamp(u, v));
-// cu, cv receive the clamped barycentric coordinates.
-__device__ inline int quad_hit(const RectArgs& a, int64_t qj, int64_t qi, double dx, double dy,
-                               double det_a, double det_b, double& cu, double& cv) {
-  const double* X = a.x;
-  const double* Y = a.y;
+struct Quad {          // corners p0 (qj, qi), p1 (qj, qi+1), p2 (qj+1, qi), p3 (qj+1, qi+1)
+  double x0, y0, x1, y1, x2, y2, x3, y3;
+};
+
+__device__ inline Quad load_quad(const RectArgs& a, int64_t qj, int64_t qi) {
   const int64_t r0 = qj * a.sy, r1 = (qj + 1) * a.sy;
-  const double p0x = X[r0 + qi], p1x = X[r0 + qi + 1], p2x = X[r1 + qi], p3x = X[r1 + qi + 1];
-  const double p0y = Y[r0 + qi], p1y = Y[r0 + qi + 1], p2y = Y[r1 + qi], p3y = Y[r1 + qi + 1];
+  return Quad{a.x[r0 + qi], a.y[r0 + qi], a.x[r0 + qi + 1], a.y[r0 + qi + 1],
+              a.x[r1 + qi], a.y[r1 + qi], a.x[r1 + qi + 1], a.y[r1 + qi + 1]};
+}
+
+// Test triangle A then B of quad q for the target pixel centre (dx, dy)
+// (rectify.py:556-573).  Returns 0 (no hit), 1 (triangle A: src = p0 +
+// clamp(u, v)) or 2 (triangle B: src = p3 - clamp(u, v)); cu, cv receive the
+// clamped barycentric coordinates.
+__device__ inline int quad_hit(const RectArgs& a, const Quad& q, double dx, double dy,
+                               double det_a, double det_b, double& cu, double& cv) {
   const double umin = -a.uv_delta, vmin = -a.uv_delta, uvmax = 1.0 + 2 * a.uv_delta;
   if (det_a != 0.0) {
-    const double u = fu(dx, dy, p0x, p0y, p2x, p2y) / det_a;
-    const double v = fv(dx, dy, p0x, p0y, p1x, p1y) / det_a;
+    const double u = fu(dx, dy, q.x0, q.y0, q.x2, q.y2) / det_a;
+    const double v = fv(dx, dy, q.x0, q.y0, q.x1, q.y1) / det_a;
     if (u >= umin && v >= vmin && u + v <= uvmax) {
       cu = fclamp(u, 0.0, 1.0);
       cv = fclamp(v, 0.0, 1.0);
@@ -223,8 +228,8 @@ __device__ inline int quad_hit(const RectArgs& a, int64_t qj, int64_t qi, double
     }
   }
   if (det_b != 0.0) {
-    const double u = fu(dx, dy, p3x, p3y, p1x, p1y) / det_b;
-    const double v = fv(dx, dy, p3x, p3y, p2x, p2y) / det_b;
+    const double u = fu(dx, dy, q.x3, q.y3, q.x1, q.y1) / det_b;
+    const double v = fv(dx, dy, q.x3, q.y3, q.x2, q.y2) / det_b;
     if (u >= umin && v >= vmin && u + v <= uvmax) {
       cu = fclamp(u, 0.0, 1.0);
       cv = fclamp(v, 0.0, 1.0);
@@ -234,46 +239,71 @@ __device__ inline int quad_hit(const RectArgs& a, int64_t qj, int64_t qi, double
   return 0;
 }
 
-__device__ inline void quad_dets(const RectArgs& a, int64_t qj, int64_t qi, double& det_a,
-                                 double& det_b) {
-  const int64_t r0 = qj * a.sy, r1 = (qj + 1) * a.sy;
-  const double p0x = a.x[r0 + qi], p1x = a.x[r0 + qi + 1], p2x = a.x[r1 + qi],
-               p3x = a.x[r1 + qi + 1];
-  const double p0y = a.y[r0 + qi], p1y = a.y[r0 + qi + 1], p2y = a.y[r1 + qi],
-               p3y = a.y[r1 + qi + 1];
-  det_a = fdet(p0x, p0y, p1x, p1y, p2x, p2y);
+__device__ inline void quad_dets(const Quad& q, double& det_a, double& det_b) {
+  det_a = fdet(q.x0, q.y0, q.x1, q.y1, q.x2, q.y2);
   if (det_a != det_a) det_a = 0.0;
-  det_b = fdet(p3x, p3y, p2x, p2y, p1x, p1y);
+  det_b = fdet(q.x3, q.y3, q.x2, q.y2, q.x1, q.y1);
   if (det_b != det_b) det_b = 0.0;
 }
 
+// target pixel (column, row) of a source point relative to a tile, as
+// np.floor(...).astype(np.int64) (rectify.py:500-501)
+__device__ inline int64_t pix_i(const RectArgs& a, const TileInfo& ti, double x) {
+  return f64_to_i64_x86(floor((x - ti.x_off) / a.x_scale));
+}
+__device__ inline int64_t pix_j(const RectArgs& a, const TileInfo& ti, double y) {
+  return f64_to_i64_x86(floor((y - ti.y_off) / a.y_scale));
+}
+
 // ---- K5a: claim target pixels with the raster-order key of hitting quads -------
+// Lanes take consecutive quads of a window row: the right-hand corners (p1,
+// p3) of a quad are the left-hand corners (p0, p2) of the next lane's quad, so
+// their coordinates and target-pixel indices (two float64 divisions each)
+// come from the neighbour lane by a shuffle; only the last quad of a row or of
+// the wave loads/computes them itself.
 template <bool PREREAD>
 __global__ void __launch_bounds__(kThreads)
 rectify_claim_kernel(RectArgs a) {
+  const int lane = threadIdx.x & 63;
   for (int64_t c = blockIdx.x; c < a.nchunks; c += gridDim.x) {
     const TileInfo ti = a.tiles[a.chunk_tile[c]];
     const int64_t nq_i = ti.swin - 1;
     const int64_t q = a.chunk_q0[c] + threadIdx.x;
-    if (ti.si0 < 0 || nq_i <= 0 || q >= nq_i * (int64_t)(ti.shin - 1)) continue;
-    const int64_t lj = q / nq_i, li = q - lj * nq_i;       // quad within the tile window
-    const int64_t qj = ti.sj0 + lj, qi = ti.si0 + li;       // global quad corner p0
-    const int64_t r0 = qj * a.sy, r1 = (qj + 1) * a.sy;
-    const double px[4] = {a.x[r0 + qi], a.x[r0 + qi + 1], a.x[r1 + qi], a.x[r1 + qi + 1]};
-    const double py[4] = {a.y[r0 + qi], a.y[r0 + qi + 1], a.y[r1 + qi], a.y[r1 + qi + 1]};
-    int64_t imin = INT64_MAX, imax = INT64_MIN, jmin = INT64_MAX, jmax = INT64_MIN;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {  // np.floor(...).astype(np.int64)  (rectify.py:500-501)
-      const int64_t pi = f64_to_i64_x86(floor((px[k] - ti.x_off) / a.x_scale));
-      const int64_t pj = f64_to_i64_x86(floor((py[k] - ti.y_off) / a.y_scale));
-      imin = min(imin, pi); imax = max(imax, pi);
-      jmin = min(jmin, pj); jmax = max(jmax, pj);
+    const bool valid = ti.si0 >= 0 && nq_i > 0 && q < nq_i * (int64_t)(ti.shin - 1);
+    int64_t lj = 0, li = 0, qj = 0, qi = 0;
+    Quad Q{NAN, NAN, NAN, NAN, NAN, NAN, NAN, NAN};
+    int64_t pi0 = 0, pj0 = 0, pi2 = 0, pj2 = 0;
+    if (valid) {
+      lj = q / nq_i;
+      li = q - lj * nq_i;                     // quad within the tile window
+      qj = ti.sj0 + lj;
+      qi = ti.si0 + li;                       // global quad corner p0
+      const int64_t r0 = qj * a.sy, r1 = (qj + 1) * a.sy;
+      Q.x0 = a.x[r0 + qi]; Q.y0 = a.y[r0 + qi];
+      Q.x2 = a.x[r1 + qi]; Q.y2 = a.y[r1 + qi];
+      pi0 = pix_i(a, ti, Q.x0); pj0 = pix_j(a, ti, Q.y0);
+      pi2 = pix_i(a, ti, Q.x2); pj2 = pix_j(a, ti, Q.y2);
     }
+    // right-hand corners from the next lane (all lanes take part in shuffles)
+    Q.x1 = __shfl_down(Q.x0, 1, 64); Q.y1 = __shfl_down(Q.y0, 1, 64);
+    Q.x3 = __shfl_down(Q.x2, 1, 64); Q.y3 = __shfl_down(Q.y2, 1, 64);
+    int64_t pi1 = __shfl_down(pi0, 1, 64), pj1 = __shfl_down(pj0, 1, 64);
+    int64_t pi3 = __shfl_down(pi2, 1, 64), pj3 = __shfl_down(pj2, 1, 64);
+    if (!valid) continue;
+    if (lane == 63 || li + 1 >= nq_i) {       // neighbour lane is not quad (lj, li+1)
+      const int64_t r0 = qj * a.sy, r1 = (qj + 1) * a.sy;
+      Q.x1 = a.x[r0 + qi + 1]; Q.y1 = a.y[r0 + qi + 1];
+      Q.x3 = a.x[r1 + qi + 1]; Q.y3 = a.y[r1 + qi + 1];
+      pi1 = pix_i(a, ti, Q.x1); pj1 = pix_j(a, ti, Q.y1);
+      pi3 = pix_i(a, ti, Q.x3); pj3 = pix_j(a, ti, Q.y3);
+    }
+    int64_t imin = min(min(pi0, pi1), min(pi2, pi3)), imax = max(max(pi0, pi1), max(pi2, pi3));
+    int64_t jmin = min(min(pj0, pj1), min(pj2, pj3)), jmax = max(max(pj0, pj1), max(pj2, pj3));
     if (imax < 0 || jmax < 0 || imin >= ti.tw || jmin >= ti.th) continue;
     imin = max(imin, (int64_t)0); jmin = max(jmin, (int64_t)0);
     imax = min(imax, (int64_t)ti.tw - 1); jmax = min(jmax, (int64_t)ti.th - 1);
     double det_a, det_b;
-    quad_dets(a, qj, qi, det_a, det_b);
+    quad_dets(Q, det_a, det_b);
     if (det_a == 0.0 && det_b == 0.0) continue;
     const uint32_t key = (uint32_t)(qj * a.w + qi);
     for (int64_t dj = jmin; dj <= jmax; ++dj) {
@@ -283,7 +313,7 @@ rectify_claim_kernel(RectArgs a) {
         if (PREREAD && krow[di] <= key) continue;  // already claimed by an earlier quad
         const double dx = ti.x_off + ((double)di + 0.5) * a.x_scale;
         double cu, cv;
-        if (quad_hit(a, qj, qi, dx, dy, det_a, det_b, cu, cv)) atomicMin(&krow[di], key);
+        if (quad_hit(a, Q, dx, dy, det_a, det_b, cu, cv)) atomicMin(&krow[di], key);
       }
     }
   }
@@ -303,13 +333,14 @@ rectify_resolve_kernel(RectArgs a, int64_t ntiles_x) {
       const int64_t t = (r / ti0.th) * ntiles_x + c / ti0.tw;  // tile 0 has the full tile size
       const TileInfo ti = a.tiles[t];
       const int64_t qj = key / a.w, qi = key - qj * a.w;
+      const Quad Q = load_quad(a, qj, qi);
       double det_a, det_b;
-      quad_dets(a, qj, qi, det_a, det_b);
+      quad_dets(Q, det_a, det_b);
       const int64_t dj = r - ti.r0, di = c - ti.c0;
       const double dy = ti.y_off + ((double)dj + 0.5) * a.y_scale;
       const double dx = ti.x_off + ((double)di + 0.5) * a.x_scale;
       double cu, cv;
-      const int tri = quad_hit(a, qj, qi, dx, dy, det_a, det_b, cu, cv);
+      const int tri = quad_hit(a, Q, dx, dy, det_a, det_b, cu, cv);
       if (tri) {
         const int64_t li = qi - ti.si0, lj = qj - ti.sj0;   // tile-local quad indices
         double src_i, src_j;
