@@ -57,6 +57,8 @@ extern "C" {
 /* ---- err_flags bits ------------------------------------------------------ */
 #define XRS_EFLAG_INDEX 1     /* numpy IndexError (window index out of range) */
 #define XRS_EFLAG_BAND 2      /* read outside the source band held on device  */
+#define XRS_EFLAG_NAN_TO_INT 4  /* int(nan): coarsen mode on a float chunk with NaN (ValueError) */
+#define XRS_EFLAG_INF_TO_INT 8  /* int(+-inf): coarsen mode, infinite values (OverflowError)   */
 
 /* library identification */
 const char* xrs_version(void);
@@ -121,6 +123,10 @@ int xrs_reproject(const void* src, int src_dtype, int64_t n, int64_t src_h,
 #define XRS_AGG_FIRST 7
 #define XRS_AGG_LAST 8
 #define XRS_AGG_CENTER 9
+#define XRS_AGG_MEDIAN 10     /* xrs_coarsen only (the fused xrs_affine path: 1..9) */
+#define XRS_AGG_MODE 11
+#define XRS_AGG_STD 12
+#define XRS_AGG_VAR 13
 
 /* -------------------------------------------------------------------------
  * xrs_affine — replaces affine._upscale (affine.py:316-362), i.e.
@@ -154,6 +160,40 @@ int xrs_affine(const void* src, int src_dtype, int64_t nt, int64_t src_h, int64_
                int64_t chunk_x, const int64_t* rel_x, const int64_t* len_x,
                const double* off_x, const int64_t* t_next, double cval, int recover_nan,
                void* workspace, int64_t workspace_bytes, void* stream);
+
+/* -------------------------------------------------------------------------
+ * xrs_coarsen — replaces da.coarsen(agg, array, {ndim-2: div_y, ndim-1:
+ * div_x}) (affine.py:308-310 -> dask chunk.coarsen -> coarsen.py:50-155),
+ * SURVEY §8(b) seam 3, for every AGG_METHODS key (constants.py:51-65):
+ * mean, sum, max, min, prod, count, first, last, center, median, mode, std,
+ * var.  Float blocks use numpy's nan-reducers; integer blocks the plain
+ * reducers with float results rint-ed and cast back (coarsen.py:91-111).
+ * src: (nt, src_h, src_w) strides (src_st, src_sy, 1), src_h % div_y == 0 and
+ *   src_w % div_x == 0 (dask's alignment check).
+ * dst: (nt, src_h/div_y, src_w/div_x) strides (dst_st, dst_sy, 1); dst_dtype
+ *   = the reducer's numpy result dtype (count, mode: int64; sum/prod of
+ *   integers: int64 bits, uint64 for unsigned sources).
+ * The dask chunking (after da.coarsen's aligned rechunk) is passed as the
+ *   chunk id of every slice / row / column: chunk_t (nt), chunk_y (src_h),
+ *   chunk_x (src_w), device int32, ids < n_chunks_*.  It matters twice:
+ *   - a window that is a whole chunk wide (chunk width == div_x) is summed as
+ *     ONE pairwise loop over its div_y*div_x values (numpy coalesces the
+ *     window axes of such a block), other windows row by row; chunk_x NULL
+ *     = the whole width is one chunk;
+ *   - mode on float sources (coarsen.py:133-139): the offset is int(min) of
+ *     the chunk holding the window, so all three id arrays, a workspace of
+ *     xrs_coarsen_workspace_size(n_chunks_t*n_chunks_y*n_chunks_x) bytes and
+ *     err_flags (NaN -> XRS_EFLAG_NAN_TO_INT, +-inf -> XRS_EFLAG_INF_TO_INT)
+ *     are required; otherwise chunk_t / chunk_y / workspace may be NULL / 0.
+ * ------------------------------------------------------------------------- */
+int64_t xrs_coarsen_workspace_size(int64_t n_chunks);
+
+int xrs_coarsen(const void* src, int src_dtype, int64_t nt, int64_t src_h, int64_t src_w,
+                int64_t src_st, int64_t src_sy, void* dst, int dst_dtype, int64_t dst_st,
+                int64_t dst_sy, int64_t div_y, int64_t div_x, int agg, const int32_t* chunk_t,
+                const int32_t* chunk_y, const int32_t* chunk_x, int64_t n_chunks_t,
+                int64_t n_chunks_y, int64_t n_chunks_x, void* workspace,
+                int64_t workspace_bytes, int32_t* err_flags, void* stream);
 
 /* *flag = 1 if any of the n elements of a float32/float64 device array is NaN
  * (da.any(da.isnan(array)), affine.py:347-349); integer dtypes -> 0. */

@@ -154,6 +154,47 @@ AGGS = {
 }
 
 
+def aligned_coarsen_chunks(chunks, multiple):
+    """dask/array/routines.py:2194-2229 (dask 2021.10)."""
+    overflow = np.array(chunks) % multiple
+    excess = overflow.sum()
+    new_chunks = np.array(chunks) - overflow
+    validity = new_chunks == chunks
+    valid_inds, invalid_inds = np.where(validity)[0], np.where(~validity)[0]
+    order = [*invalid_inds[np.argsort(new_chunks[invalid_inds])],
+             *valid_inds[np.argsort(new_chunks[valid_inds])]]
+    multiples = (multiple,) * (excess // multiple)
+    remainder = (excess % multiple,) if excess % multiple > 0 else ()
+    for idx, extra in enumerate(multiples):
+        new_chunks[order[idx]] += extra
+    new_chunks = np.array([*new_chunks, *remainder])
+    return tuple(int(c) for c in new_chunks[new_chunks > 0])
+
+
+def coarsen_chunked(agg, array, axes, chunks):
+    """dask.array.routines.coarsen (routines.py:2233-2261): rechunk to
+    aligned_coarsen_chunks, then chunk.coarsen per block (the block matters
+    for `mode`, whose offset is the block minimum, coarsen.py:133)."""
+    chunks = list(normalize_chunks(chunks, array.shape))
+    for i, div in axes.items():
+        aligned = aligned_coarsen_chunks(chunks[i], div)
+        if aligned != tuple(chunks[i]):
+            chunks[i] = aligned
+    starts = [np.cumsum((0,) + tuple(c[:-1])) for c in chunks]
+    out = None
+    for block in product(*(range(len(c)) for c in chunks)):
+        sl = tuple(slice(int(starts[d][b]), int(starts[d][b]) + chunks[d][b])
+                   for d, b in enumerate(block))
+        res = np.asarray(coarsen(agg, array[sl], dict(axes)))
+        if out is None:
+            out = np.empty(tuple(s // axes.get(i, 1) for i, s in enumerate(array.shape)),
+                           dtype=res.dtype)
+        osl = tuple(slice(s.start // axes.get(i, 1), s.stop // axes.get(i, 1))
+                    for i, s in enumerate(sl))
+        out[osl] = res
+    return out
+
+
 def coarsen(agg, array, axes):
     """dask.array.coarsen(reduction, x, axes) on one numpy block (chunk.coarsen)."""
     axes = {i: axes.get(i, 1) for i in range(array.ndim)}
@@ -208,7 +249,8 @@ def resample_array(array, affine_matrix, output_shape, output_chunks, interp, ag
              (affine_matrix[1][0], j_scale / j_div, affine_matrix[1][2]))
         shape = tuple(output_shape[:-2]) + (output_shape[-2] * j_div, output_shape[-1] * i_div)
         up = upscale(array, m, shape, output_chunks, interp, recover_nan, fill)
-        return coarsen(agg, up, {up.ndim - 2: j_div, up.ndim - 1: i_div})
+        return coarsen_chunked(agg, up, {up.ndim - 2: j_div, up.ndim - 1: i_div},
+                               output_chunks)
     return upscale(array, affine_matrix, output_shape, output_chunks, interp, recover_nan, fill)
 
 

@@ -29,6 +29,8 @@ XRS_ERR_NOTIMPL = -3
 
 XRS_EFLAG_INDEX = 1
 XRS_EFLAG_BAND = 2
+XRS_EFLAG_NAN_TO_INT = 4
+XRS_EFLAG_INF_TO_INT = 8
 
 INTERP_CODES = {"nearest": 0, "bilinear": 1, "triangular": 2}
 
@@ -77,6 +79,14 @@ _SIGNATURES = {
         _c_i64, _c_ptr, _c_ptr, _c_ptr,                                          # x chunks
         _c_ptr, _c_dbl, _c_int, _c_ptr, _c_i64, _c_ptr,                          # t_next .. stream
     ]),
+    "xrs_coarsen_workspace_size": (_c_i64, [_c_i64]),
+    "xrs_coarsen": (_c_int, [
+        _c_ptr, _c_int, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64,                  # src
+        _c_ptr, _c_int, _c_i64, _c_i64,                                          # dst
+        _c_i64, _c_i64, _c_int,                                                  # div, agg
+        _c_ptr, _c_ptr, _c_ptr, _c_i64, _c_i64, _c_i64,                          # chunk ids
+        _c_ptr, _c_i64, _c_ptr, _c_ptr,                                          # ws, flags, stream
+    ]),
     "xrs_any_nan": (_c_int, [_c_ptr, _c_int, _c_i64, _c_ptr, _c_ptr]),
     "xrs_ij_bboxes": (_c_int, [_c_ptr, _c_ptr, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64,
                                _c_ptr, _c_ptr, _c_ptr, _c_ptr]),
@@ -88,7 +98,10 @@ _SIGNATURES = {
 }
 
 AGG_CODES = {"mean": 1, "sum": 2, "max": 3, "min": 4, "prod": 5, "count": 6, "first": 7,
-             "last": 8, "center": 9}
+             "last": 8, "center": 9, "median": 10, "mode": 11, "std": 12, "var": 13}
+# reducers the fused K3 (xrs_affine) evaluates; the others run as K2 at the
+# div-x grid followed by K7 (xrs_coarsen)
+FUSED_AGGS = ("mean", "sum", "max", "min", "prod", "count", "first", "last", "center")
 
 _lib = None
 _lock = threading.Lock()

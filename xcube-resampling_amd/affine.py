@@ -128,6 +128,48 @@ def time_neighbours(nt: int, chunk: int, order: int) -> np.ndarray | None:
     return out
 
 
+def aligned_coarsen_chunks(chunks, multiple: int) -> tuple[int, ...]:
+    """dask.array.routines.aligned_coarsen_chunks (dask 2021.10: the rechunk
+    da.coarsen applies before chunk.coarsen): chunk sizes made multiples of
+    `multiple`, the excess redistributed to the smallest chunks, any remainder
+    appended."""
+    chunks = np.array(chunks, dtype=np.int64)
+    overflow = chunks % multiple
+    excess = int(overflow.sum())
+    new = chunks - overflow
+    valid = new == chunks
+    vi, ii = np.where(valid)[0], np.where(~valid)[0]
+    order = [*ii[np.argsort(new[ii])], *vi[np.argsort(new[vi])]]
+    parts = (multiple,) * (excess // multiple)
+    rem = (excess % multiple,) if excess % multiple else ()
+    for k, extra in enumerate(parts):
+        new[order[k]] += extra
+    new = np.array([*new, *rem], dtype=np.int64)
+    return tuple(int(c) for c in new[new > 0])
+
+
+def _has_whole_chunk_windows(chunk_x: np.ndarray, div_x: int) -> bool:
+    """True if some dask chunk along x is exactly one coarsen window wide."""
+    sizes = np.bincount(chunk_x)
+    return bool(np.any(sizes == div_x))
+
+
+def coarsen_chunk_ids(shape, chunks, factors):
+    """Per axis, the id of the dask chunk that holds each index after
+    da.coarsen's alignment rechunk (routines.py coarsen: aligned_coarsen_chunks
+    on every coarsened axis whose chunks are not multiples of the factor)."""
+    ids = []
+    for n, c, f in zip(shape, chunks, factors):
+        c = min(int(c), n)
+        sizes = (c,) * (n // c) + ((n % c,) if n % c else ())
+        if f > 1:
+            aligned = aligned_coarsen_chunks(sizes, f)
+            if aligned != sizes:
+                sizes = aligned
+        ids.append(np.repeat(np.arange(len(sizes), dtype=np.int32), sizes))
+    return tuple(ids)
+
+
 @dataclass
 class AffinePlan:
     out_h: int
@@ -150,6 +192,12 @@ class AffinePlan:
     cval: float
     recover_nan: bool
     out_dtype: np.dtype
+    # reducers outside the fused K3 (median, mode, std, var): K2 evaluates the
+    # div-x intermediate (out_h, out_w above are then its size), K7 coarsens it
+    post_agg: str | None = None
+    post_div: tuple[int, int] = (1, 1)
+    post_dtype: np.dtype | None = None
+    post_chunks: tuple | None = None   # dask chunk ids (t, y, x) for float mode
     _cache: dict = field(default_factory=dict, repr=False)
 
     def device_tables(self, device) -> dict:
@@ -167,7 +215,7 @@ class AffinePlan:
 def _agg_dtype(agg: str, dtype: np.dtype) -> np.dtype:
     """numpy result dtype of the coarsen reducer on a block of `dtype`."""
     dtype = np.dtype(dtype)
-    if agg == "count":
+    if agg in ("count", "mode"):   # np.count_nonzero; _mode_from_normalized's int64
         return np.dtype(np.int64)
     if np.issubdtype(dtype, np.floating):
         return dtype
@@ -201,23 +249,35 @@ def plan_affine(src_shape, dtype, affine_matrix, output_shape, output_chunks, in
         agg_name = None
     recover = bool(recover_nan and interp > 0 and np.issubdtype(dtype, np.floating))
     inter_dtype = np.dtype(np.float64) if recover else np.dtype(dtype)
+    post = {}
     if agg_name is None:
         agg_code, out_dtype = 0, inter_dtype
     else:
         if agg_name not in _native.AGG_CODES:
-            raise NotImplementedError(
-                f"aggregation method {agg_name!r} is not implemented by the engine yet")
+            raise NotImplementedError(f"aggregation method {agg_name!r} is not supported")
         agg_code, out_dtype = _native.AGG_CODES[agg_name], _agg_dtype(agg_name, inter_dtype)
+        t_chunk = output_chunks[0] if len(output_shape) == 3 else nt
+        chunks = coarsen_chunk_ids((nt, out_h * div_y, out_w * div_x),
+                                   (t_chunk, tile_h, tile_w), (1, div_y, div_x))
+        # K3 sums every window row by row; a chunk one window wide is summed
+        # as one pairwise loop by numpy (see xrs_coarsen) -> K7 handles it
+        whole = _has_whole_chunk_windows(chunks[2], div_x)
+        if agg_name not in _native.FUSED_AGGS or whole:
+            post = dict(post_agg=agg_name, post_div=(div_y, div_x),
+                        post_dtype=np.dtype(out_dtype), post_chunks=chunks)
+            agg_code, out_dtype = 0, inter_dtype
     rel_y, len_y, off_y = axis_chunk_params(scale_y, j_off, out_h * div_y, tile_h, h, interp)
     rel_x, len_x, off_x = axis_chunk_params(scale_x, i_off, out_w * div_x, tile_w, w, interp)
     t_next = None
     if len(output_shape) == 3:
         t_next = time_neighbours(nt, output_chunks[0], interp)
+    if post:  # K2 writes the intermediate (out*div, div 1), K7 reduces it
+        out_h, out_w, div_y, div_x = out_h * div_y, out_w * div_x, 1, 1
     return AffinePlan(out_h=out_h, out_w=out_w, div_y=div_y, div_x=div_x, agg_code=agg_code,
                       order=interp, scale_y=scale_y, scale_x=scale_x, chunk_y=tile_h,
                       rel_y=rel_y, len_y=len_y, off_y=off_y, chunk_x=tile_w, rel_x=rel_x,
                       len_x=len_x, off_x=off_x, t_next=t_next, cval=float(fill_value),
-                      recover_nan=recover, out_dtype=np.dtype(out_dtype))
+                      recover_nan=recover, out_dtype=np.dtype(out_dtype), **post)
 
 
 def _resample_array(data, dims, chunks, affine_matrix, output_shape, output_chunks, interp,
@@ -236,7 +296,11 @@ def _resample_array(data, dims, chunks, affine_matrix, output_shape, output_chun
     plan = plan_affine(tuple(src.shape), dtype, affine_matrix, output_shape, output_chunks,
                        interp, agg, recover, fill_value)
     out = kernels.affine(src, plan)
-    if np.dtype(plan.out_dtype) == np.uint64:
+    if plan.post_agg is not None:
+        out = kernels.coarsen(out, plan.post_div[0], plan.post_div[1], plan.post_agg,
+                              plan.post_dtype, chunk_ids=plan.post_chunks)
+    final_dtype = plan.out_dtype if plan.post_dtype is None else plan.post_dtype
+    if np.dtype(final_dtype) == np.uint64:
         out = out.cpu().numpy().view(np.uint64)
         return out[0] if expanded else out
     return out[0] if expanded else out

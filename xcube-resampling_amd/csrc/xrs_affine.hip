@@ -125,13 +125,6 @@ template <> struct ScipyOut<double> {
   __device__ static inline double cast(double t) { return t; }
 };
 
-template <typename T> __device__ inline bool is_nan(T v) { return false; }
-template <> __device__ inline bool is_nan<float>(float v) { return v != v; }
-template <> __device__ inline bool is_nan<double>(double v) { return v != v; }
-template <typename T> __device__ inline bool is_finite(T v) { return true; }
-template <> __device__ inline bool is_finite<float>(float v) { return v - v == 0.0f; }
-template <> __device__ inline bool is_finite<double>(double v) { return v - v == 0.0; }
-
 enum Agg : int {
   AGG_NONE = 0, AGG_MEAN = 1, AGG_SUM = 2, AGG_MAX = 3, AGG_MIN = 4, AGG_PROD = 5,
   AGG_COUNT = 6, AGG_FIRST = 7, AGG_LAST = 8, AGG_CENTER = 9,
@@ -150,47 +143,6 @@ struct AffineArgs {
   const AxisTab* ytab;     // (out_h*dy) entries
   const AxisTab* xtab;     // (out_w*dx) entries
 };
-
-// numpy's float add.reduce of one contiguous window row (pairwise_sum):
-// n < 8 sequential from -0.0; 8 <= n <= 128 eight accumulators (static
-// indices: the blocks of 8 are unrolled), combined pairwise, then the tail.
-// `val(i)` returns element i (already NaN-replaced by the caller).
-template <typename A, typename F>
-__device__ inline A pairwise_row(int n, F&& val) {
-  if (n < 8) {
-    A s = (A)-0.0;
-    for (int i = 0; i < n; ++i) s = s + val(i);
-    return s;
-  }
-  A r[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) r[j] = val(j);
-  const int full = n - (n % 8);
-  int i = 8;
-  for (; i < full; i += 8) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) r[j] = r[j] + val(i + j);
-  }
-  A s = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
-  for (; i < n; ++i) s = s + val(i);
-  return s;
-}
-
-__device__ inline void store_any(void* dst, int64_t idx, int dtype, double fv, int64_t iv,
-                                 bool is_int) {
-  switch (dtype) {
-    case XRS_DTYPE_F32: static_cast<float*>(dst)[idx] = (float)fv; break;
-    case XRS_DTYPE_F64: static_cast<double*>(dst)[idx] = fv; break;
-    case XRS_DTYPE_I64: static_cast<int64_t*>(dst)[idx] = is_int ? iv : (int64_t)fv; break;
-    case XRS_DTYPE_U8: static_cast<uint8_t*>(dst)[idx] = (uint8_t)iv; break;
-    case XRS_DTYPE_I8: static_cast<int8_t*>(dst)[idx] = (int8_t)iv; break;
-    case XRS_DTYPE_U16: static_cast<uint16_t*>(dst)[idx] = (uint16_t)iv; break;
-    case XRS_DTYPE_I16: static_cast<int16_t*>(dst)[idx] = (int16_t)iv; break;
-    case XRS_DTYPE_U32: static_cast<uint32_t*>(dst)[idx] = (uint32_t)iv; break;
-    case XRS_DTYPE_I32: static_cast<int32_t*>(dst)[idx] = (int32_t)iv; break;
-    default: break;
-  }
-}
 
 // Source access: global memory (slice t and its zero-weight time neighbour
 // t1).  The out-of-bounds marker (-1) is clamped to a valid element; eval()

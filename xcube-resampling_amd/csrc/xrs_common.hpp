@@ -94,6 +94,80 @@ __device__ inline XcdSlice xcd_slice(int64_t nwork) {
   return s;
 }
 
+// ---- numpy reduction helpers (K3 / coarsen) --------------------------------
+template <typename T> __device__ inline bool is_nan(T v) { return false; }
+template <> __device__ inline bool is_nan<float>(float v) { return v != v; }
+template <> __device__ inline bool is_nan<double>(double v) { return v != v; }
+template <typename T> __device__ inline bool is_finite(T v) { return true; }
+template <> __device__ inline bool is_finite<float>(float v) { return v - v == 0.0f; }
+template <> __device__ inline bool is_finite<double>(double v) { return v - v == 0.0; }
+
+// numpy's float add.reduce of one contiguous window row (pairwise_sum):
+// n < 8 sequential from -0.0; 8 <= n <= 128 eight accumulators (static
+// indices: the blocks of 8 are unrolled), combined pairwise, then the tail.
+// `val(i)` returns element i (already NaN-replaced by the caller).
+template <typename A, typename F>
+__device__ inline A pairwise_row(int n, F&& val) {
+  if (n < 8) {
+    A s = (A)-0.0;
+    for (int i = 0; i < n; ++i) s = s + val(i);
+    return s;
+  }
+  A r[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = val(j);
+  const int full = n - (n % 8);
+  int i = 8;
+  for (; i < full; i += 8) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = r[j] + val(i + j);
+  }
+  A s = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+  for (; i < n; ++i) s = s + val(i);
+  return s;
+}
+
+// numpy's full pairwise_sum (loops_utils.h.src): blocks of <= 128 as above,
+// longer runs split at n2 = n/2 - (n/2)%8 and the halves summed recursively.
+template <typename A, typename F>
+__device__ A pairwise_sum(int off, int n, F&& val) {
+  if (n <= 128) return pairwise_row<A>(n, [&](int i) { return val(off + i); });
+  int n2 = n / 2;
+  n2 -= n2 % 8;
+  const A lo = pairwise_sum<A>(off, n2, val);
+  return lo + pairwise_sum<A>(off + n2, n - n2, val);
+}
+
+// numpy add.reduce over the window axes (1, 3) of dask chunk.coarsen's
+// (h/dy, dy, w/dx, dx) block, starting from the identity 0: each window row is
+// one inner pairwise loop, rows accumulated in order — unless the block is a
+// single window wide (chunk width == dx), where nditer coalesces the two axes
+// into ONE pairwise loop over all dy*dx values (row-major).
+template <typename A, typename F>
+__device__ inline A window_sum(bool whole, int ny, int nx, F&& val2d) {
+  if (whole) return (A)0.0 + pairwise_sum<A>(0, ny * nx, [&](int i) { return val2d(i / nx, i % nx); });
+  A t = (A)0.0;
+  for (int r = 0; r < ny; ++r)
+    t = t + pairwise_sum<A>(0, nx, [&](int c) { return val2d(r, c); });
+  return t;
+}
+
+__device__ inline void store_any(void* dst, int64_t idx, int dtype, double fv, int64_t iv,
+                                 bool is_int) {
+  switch (dtype) {
+    case XRS_DTYPE_F32: static_cast<float*>(dst)[idx] = (float)fv; break;
+    case XRS_DTYPE_F64: static_cast<double*>(dst)[idx] = fv; break;
+    case XRS_DTYPE_I64: static_cast<int64_t*>(dst)[idx] = is_int ? iv : (int64_t)fv; break;
+    case XRS_DTYPE_U8: static_cast<uint8_t*>(dst)[idx] = (uint8_t)iv; break;
+    case XRS_DTYPE_I8: static_cast<int8_t*>(dst)[idx] = (int8_t)iv; break;
+    case XRS_DTYPE_U16: static_cast<uint16_t*>(dst)[idx] = (uint16_t)iv; break;
+    case XRS_DTYPE_I16: static_cast<int16_t*>(dst)[idx] = (int16_t)iv; break;
+    case XRS_DTYPE_U32: static_cast<uint32_t*>(dst)[idx] = (uint32_t)iv; break;
+    case XRS_DTYPE_I32: static_cast<int32_t*>(dst)[idx] = (int32_t)iv; break;
+    default: break;
+  }
+}
+
 template <typename F>
 inline int dispatch_dtype(int dtype, F&& f) {
   switch (dtype) {

@@ -32,6 +32,11 @@ class ErrorFlags:
             raise IndexError(f"{what}: index out of bounds for the source window")
         if bits & _native.XRS_EFLAG_BAND:
             raise _native.NativeLibraryError(f"{what}: read outside the device's source band")
+        # coarsen.py:133-134: int(flat.min()) / int(flat.max()) on a float chunk
+        if bits & _native.XRS_EFLAG_NAN_TO_INT:
+            raise ValueError("cannot convert float NaN to integer")
+        if bits & _native.XRS_EFLAG_INF_TO_INT:
+            raise OverflowError("cannot convert float infinity to integer")
 
 
 def reproject(src, plan, interp: str, fill: float, out_dtype=None, rows=None, out=None,
@@ -257,4 +262,50 @@ def affine(src, plan, out=None, stream=None):
         ptr(tabs["t_next"]) if tabs["t_next"] is not None else None,
         float(plan.cval), int(plan.recover_nan), ptr(ws), nbytes, stream_handle(device, stream))
     _native.check(rc, "xrs_affine")
+    return out
+
+
+def coarsen(src, div_y: int, div_x: int, agg: str, out_dtype, chunk_ids=None, out=None,
+            stream=None):
+    """K7 — da.coarsen(agg, src, {1: div_y, 2: div_x}) on a device tensor
+    (nt, H, W) (affine.py:308-310 -> dask chunk.coarsen -> coarsen.py).
+
+    chunk_ids: for ``mode`` on float data, the dask chunk id of every slice,
+    row and column: ``(ct, cy, cx)`` int32 numpy arrays (coarsen.py:133 takes
+    the offset from the chunk minimum).  Returns (nt, H/div_y, W/div_x) in
+    ``out_dtype`` (uint64 results are produced as int64 bits).
+    """
+    device = src.device
+    code = _native.AGG_CODES.get(agg)
+    if code is None:
+        raise NotImplementedError(f"aggregation method {agg!r} is not supported")
+    nt, h, w = src.shape
+    if h % div_y or w % div_x:
+        raise ValueError(f"Coarsening factors {{1: {div_y}, 2: {div_x}}} do not align with "
+                         f"array shape {tuple(src.shape)}.")
+    if out is None:
+        out = empty((nt, h // div_y, w // div_x), out_dtype, device)
+    st, sy, sx = src.stride()
+    dt, dy, dx = out.stride()
+    if sx != 1 or dx != 1:
+        raise ValueError("innermost dimension must be contiguous")
+    out_code = _native.dtype_code(np.int64 if np.dtype(out_dtype) == np.uint64 else out_dtype)
+    lib = _native.lib()
+    flags = ErrorFlags(device)
+    ct = cy = cx = None
+    ncounts = (0, 0, 0)
+    ws, ws_bytes = None, 0
+    if chunk_ids is not None:
+        ct, cy, cx = (to_device(np.ascontiguousarray(c, np.int32), device) for c in chunk_ids)
+        ncounts = tuple(int(np.max(c)) + 1 for c in chunk_ids)
+        ws_bytes = lib.xrs_coarsen_workspace_size(ncounts[0] * ncounts[1] * ncounts[2])
+        ws = torch().empty(max(ws_bytes, 1), dtype=torch().uint8, device=device)
+    rc = lib.xrs_coarsen(
+        ptr(src), _native.DTYPE_CODES[_np_dtype(src)], nt, h, w, st, sy, ptr(out), out_code, dt,
+        dy, div_y, div_x, code, ptr(ct) if ct is not None else None,
+        ptr(cy) if cy is not None else None, ptr(cx) if cx is not None else None, *ncounts,
+        ptr(ws) if ws is not None else None, ws_bytes, flags.ptr, stream_handle(device, stream))
+    _native.check(rc, "xrs_coarsen")
+    if code == _native.AGG_CODES["mode"]:
+        flags.raise_if_set("coarsen")
     return out
