@@ -175,3 +175,32 @@ def test_integral_grid_coarsen_special_values(dtype, nd, agg):
         got = A._resample_array(a, None, None, m, lead + oshape, ochunks, 1, agg, False, fill)
         got = got if isinstance(got, np.ndarray) else got.cpu().numpy()
         assert_bitwise_equal(got, np.asarray(ref), f"{dtype} {agg} {m}")
+
+
+@pytest.mark.parametrize("stage", ["0", "1"])
+def test_reduce_lds_stage_knob_bit_identical(stage, monkeypatch):
+    """K3 with the tile source footprint staged in LDS (XRS_AFFINE_STAGE=1) and
+    with direct global taps give the same bits as the oracle (random scales,
+    2-D / 3-D, NaN, recover_nans)."""
+    import xcube_resampling_amd.affine as A
+    from oracle import affine_ref
+
+    monkeypatch.setenv("XRS_AFFINE_STAGE", stage)
+    for seed in range(8):
+        rng = np.random.default_rng(7000 + seed)
+        dtype = [np.float32, np.float64, np.int16, np.uint8][seed % 4]
+        nd = 3 if seed % 2 else 2
+        a = _random_case(rng, dtype, nd, 0.02)
+        s_i = float(rng.choice([2.0, 2.5, 4.0, 3.0]))
+        s_j = float(rng.choice([2.0, 3.0, 4.0, 1.5]))
+        m = ((s_i, 0.0, float(rng.uniform(-2, 2))), (0.0, s_j, float(rng.choice([0.0, 0.5]))))
+        lead = a.shape[:-2]
+        oshape = lead + (int(rng.integers(5, 30)), int(rng.integers(5, 30)))
+        ochunks = tuple(1 for _ in lead) + (int(rng.integers(4, 16)), int(rng.integers(4, 16)))
+        fill = np.nan if np.issubdtype(dtype, np.floating) else 7
+        agg = ["mean", "sum", "max", "min", "count", "prod"][seed % 6]
+        recover = bool(seed % 3 == 0 and np.issubdtype(dtype, np.floating))
+        ref = affine_ref.resample_array(a, m, oshape, ochunks, 1, agg, recover, fill)
+        got = A._resample_array(a, None, None, m, oshape, ochunks, 1, agg, recover, fill)
+        got = got if isinstance(got, np.ndarray) else got.cpu().numpy()
+        assert_bitwise_equal(got, np.asarray(ref), f"stage={stage} seed {seed} {agg}")

@@ -32,6 +32,7 @@
 // nearest picks and lerp weights are bit-identical to numpy's.
 
 #include <cstdlib>
+#include <type_traits>
 
 #include "xrs_common.hpp"
 
@@ -549,6 +550,168 @@ gather_2d_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t bands_per_til
   if (eflags) atomicOr(g.err_flags, eflags);
 }
 
+// ---- K1s: LDS-staged separable gather ------------------------------------
+// The source footprint of a work item (rows [rmin, rmax] x columns [cmin,
+// cmax] of every valid tap) is read ONCE with 16-byte loads per lane — the
+// access shape of a streaming copy, ≈ 2 KB contiguous per row — and parked in
+// LDS; the per-pixel taps (irregular, 4 per bilinear pixel) are then gathered
+// from LDS instead of as 4-byte global loads.  Spans come from the entries
+// already in registers (wave shuffles + one LDS exchange).  Items whose span
+// does not fit (window wrap-around, extreme scales) take the direct path.
+template <typename T>
+__device__ inline int32_t wave_min(int32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o));
+  return v;
+}
+__device__ inline int32_t wave_max_i(int32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o));
+  return v;
+}
+
+template <typename T, typename O, int INTERP, bool VEC, int PX = 2>
+__global__ void __launch_bounds__(kThreads)
+gather_staged_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t bands_per_tile,
+                     int64_t segs_per_tile, int64_t nwork, int lds_cap) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  T* stage = reinterpret_cast<T*>(smem);
+  __shared__ int32_t part[4][4];
+  __shared__ AxisEntry rows_s[64];   // the band's row entries (band <= 64)
+  constexpr int E = VEC ? 16 / (int)sizeof(T) : 1;   // elements per staging load
+  const Geometry& g = a.g;
+  const T fill = Conv<T>::from_f64(a.fill);
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / 64), lane = threadIdx.x % 64;
+  const XcdSlice sl = xcd_slice(nwork);
+  for (int64_t w = sl.first; w < sl.end; w += sl.step) {
+    WorkItem it;
+    if (!work_item(g, w, ty0, nsegs, bands_per_tile, segs_per_tile, it)) continue;
+    const AxisEntry* xt = a.xtab + it.t * g.tile_w + (it.c0 - it.tx * g.tile_w);
+    const int ncols = (int)(it.c1 - it.c0);
+    int32_t cf[PX], cc[PX];
+    double dx[PX];
+    int32_t lo = INT32_MAX, hi = -1;
+#pragma unroll
+    for (int k = 0; k < PX; ++k) {
+      const int lc = (int)threadIdx.x + k * kThreads;
+      AxisEntry e{-1, -1, 0.0};
+      if (lc < ncols) e = xt[lc];
+      cf[k] = e.f;
+      cc[k] = e.c;
+      dx[k] = e.d;
+      if (e.f >= 0) { lo = min(lo, e.f); hi = max(hi, e.f); }
+      if (INTERP != XRS_INTERP_NEAREST && e.c >= 0) { lo = min(lo, e.c); hi = max(hi, e.c); }
+    }
+    const AxisEntry* yt = a.ytab + it.t * g.tile_h - it.ty * g.tile_h;
+    const int nrows = (int)(it.r1 - it.r0);
+    int32_t rlo = INT32_MAX, rhi = -1;
+    for (int q = lane; q < nrows; q += 64) {   // rows: every wave, same answer
+      const AxisEntry e = yt[it.r0 + q];
+      if (wave == 0) rows_s[q] = e;
+      if (e.f >= 0) { rlo = min(rlo, e.f); rhi = max(rhi, e.f); }
+      if (INTERP != XRS_INTERP_NEAREST && e.c >= 0) { rlo = min(rlo, e.c); rhi = max(rhi, e.c); }
+    }
+    lo = wave_min<T>(lo);
+    hi = wave_max_i(hi);
+    if (lane == 0) { part[wave][0] = lo; part[wave][1] = hi; }
+    __syncthreads();   // also: the previous item's gathers from `stage` are done
+    lo = min(min(part[0][0], part[1][0]), min(part[2][0], part[3][0]));
+    hi = max(max(part[0][1], part[1][1]), max(part[2][1], part[3][1]));
+    rlo = wave_min<T>(rlo);
+    rhi = wave_max_i(rhi);
+    const int cs = lo - lo % E;                             // 16-byte aligned start
+    const int ce = hi < 0 ? cs : ((hi + 1 + E - 1) / E) * E;   // exclusive, aligned
+    const int pitch = max(ce - cs, 0);
+    const int nr = rhi - rlo + 1;
+    const bool staged = hi >= 0 && rhi >= 0 && (int64_t)nr * pitch * (int64_t)sizeof(T) <= lds_cap;
+    __syncthreads();   // everyone has read `part` before the next item rewrites it
+    if (staged) {
+      // wave-uniform (row, pass) schedule: 8 loads per lane in flight, then stores
+      const int nvec = pitch / E;
+      const int passes = (nvec + 63) / 64;
+      const int rows_w = (nr - wave + 3) / 4;            // rows of this wave
+      const int nitems = rows_w * passes;
+      for (int i0 = 0; i0 < nitems; i0 += 8) {
+        using V = typename std::conditional<VEC, uint4, T>::type;
+        V tmp[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int i = i0 + u;
+          const int r = wave + 4 * (i / passes), vi = (i % passes) * 64 + lane;
+          if (i < nitems && vi < nvec) {
+            const T* gp = static_cast<const T*>(a.src) + (int64_t)(rlo + r) * a.src_sy + cs + vi * E;
+            tmp[u] = *reinterpret_cast<const V*>(gp);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int i = i0 + u;
+          const int r = wave + 4 * (i / passes), vi = (i % passes) * 64 + lane;
+          if (i < nitems && vi < nvec)
+            *reinterpret_cast<V*>(stage + r * pitch + vi * E) = tmp[u];
+        }
+      }
+      __syncthreads();
+    }
+    // (a.n > 1 re-stages per slice below; the bench and configs use n = 1)
+    for (int64_t sn = 0; sn < a.n; ++sn) {
+      const T* __restrict__ src = static_cast<const T*>(a.src) + sn * a.src_sn;
+      O* __restrict__ dst = static_cast<O*>(a.dst) + sn * a.dst_sn - g.row_begin * a.dst_sy + it.c0;
+      if (sn > 0 && staged) {
+        __syncthreads();
+        const int nvec = pitch / E;
+        for (int e = threadIdx.x; e < nr * nvec; e += kThreads) {
+          const int r = e / nvec, vi = e - r * nvec;
+          using V = typename std::conditional<VEC, uint4, T>::type;
+          *reinterpret_cast<V*>(stage + r * pitch + vi * E) =
+              *reinterpret_cast<const V*>(src + (int64_t)(rlo + r) * a.src_sy + cs + vi * E);
+        }
+        __syncthreads();
+      }
+      for (int64_t r = it.r0; r < it.r1; ++r) {
+        const AxisEntry ye = rows_s[r - it.r0];   // LDS broadcast, no global round trip
+        const bool okf = ye.f >= 0, okc = ye.c >= 0;
+        T v[4][PX];
+        if (staged) {
+          const T* lf = stage + (okf ? ye.f - rlo : 0) * pitch - cs;
+          const T* lcr = stage + (okc ? ye.c - rlo : 0) * pitch - cs;
+#pragma unroll
+          for (int k = 0; k < PX; ++k) {
+            const int32_t f = cf[k] >= 0 ? cf[k] : cs, c = cc[k] >= 0 ? cc[k] : cs;
+            v[0][k] = lf[f];
+            if (INTERP != XRS_INTERP_NEAREST) { v[1][k] = lf[c]; v[2][k] = lcr[f]; v[3][k] = lcr[c]; }
+          }
+        } else {
+          const T* rf = src + (int64_t)max(ye.f, 0) * a.src_sy;
+          const T* rc = src + (int64_t)max(ye.c, 0) * a.src_sy;
+#pragma unroll
+          for (int k = 0; k < PX; ++k) {
+            const int32_t f = max(cf[k], 0), c = max(cc[k], 0);
+            v[0][k] = rf[f];
+            if (INTERP != XRS_INTERP_NEAREST) { v[1][k] = rf[c]; v[2][k] = rc[f]; v[3][k] = rc[c]; }
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < PX; ++k) {
+          const int lc = (int)threadIdx.x + k * kThreads;
+          const bool xf = cf[k] >= 0, xc = cc[k] >= 0;
+          const T v00 = (okf && xf) ? v[0][k] : fill;
+          O out;
+          if (INTERP == XRS_INTERP_NEAREST) {
+            out = (O)v00;
+          } else {
+            const T v01 = (okf && xc) ? v[1][k] : fill;
+            const T v10 = (okc && xf) ? v[2][k] : fill;
+            const T v11 = (okc && xc) ? v[3][k] : fill;
+            out = Conv<O>::from_f64(interp4<T, INTERP>(v00, v01, v10, v11, dx[k], ye.d));
+          }
+          if (lc < ncols) __builtin_nontemporal_store(out, &dst[r * a.dst_sy + lc]);
+        }
+      }
+    }
+  }
+}
+
 // Separable gather variant (XRS_REPROJECT_VARIANT, for A/B measurements; all
 // variants are bit-identical, only the load schedule differs):
 //   0      rows carried in registers (fewest loads, one source row in flight)
@@ -557,9 +720,14 @@ gather_2d_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t bands_per_til
 //   6/7    bilinear with source-row lerp reuse (7: also skips reused loads)
 //   9/10/11  as 4 with 2/8/1 columns per thread (512/2048/256-column items)
 //   12/13  8/16 rows in flight, 2 columns per thread, non-temporal stores
+//   14     LDS-staged footprint (16-byte staging loads, taps gathered from LDS)
 // Default 12.  Interleaved A/B on one MI355X, 40960^2 bilinear, one work item
 // per block: 12 = 2.51 ms, 9 = 2.57, 4 = 2.76, 11 = 2.96, 13 = 3.69
 // (scripts/ab_reproject.py; absolute times vary ~10 % between boxes).
+// 14 (unpipelined: entries -> stage -> gather are dependent round trips per
+// item, 40 KB of LDS caps residency at 3 blocks/CU) = 7.9-11 ms for bands of
+// 6-16 rows vs 2.73 ms for 12 in the same run: kept for reference, a
+// double-buffered stage is the way to make it pay.
 inline int variant() {
   const char* v = getenv("XRS_REPROJECT_VARIANT");
   return v ? atoi(v) : 12;
@@ -572,10 +740,11 @@ int launch(const GatherArgs& a, int coord_mode, AxisEntry* xtab, AxisEntry* ytab
   const int64_t ty0 = g.row_begin / g.tile_h, ty1 = (g.row_end - 1) / g.tile_h + 1;
   const char* band_env = getenv("XRS_REPROJECT_BAND");  // A/B knob (target rows per item)
   GatherArgs args = a;
-  args.g.band = band_env && atoi(band_env) > 0 ? atoi(band_env) : kBand;
+  args.g.band = band_env && atoi(band_env) > 0 ? atoi(band_env) : (variant() == 14 ? 8 : kBand);
+  if (variant() == 14 && args.g.band > 64) args.g.band = 64;   // rows_s capacity
   const int64_t bands_per_tile = (g.tile_h + args.g.band - 1) / args.g.band;
   const int v = variant();
-  args.g.segw = kThreads * (v == 9 || v == 12 || v == 13 ? 2 : v == 10 ? 8 : v == 11 ? 1 : kPx);
+  args.g.segw = kThreads * (v == 9 || v == 12 || v == 13 || v == 14 ? 2 : v == 10 ? 8 : v == 11 ? 1 : kPx);
   const int64_t segs_per_tile = (g.tile_w + args.g.segw - 1) / args.g.segw;
   const int64_t nsegs = g.ntiles_x * segs_per_tile;
   const int64_t nwork = (ty1 - ty0) * bands_per_tile * nsegs;
@@ -634,7 +803,23 @@ int launch(const GatherArgs& a, int coord_mode, AxisEntry* xtab, AxisEntry* ytab
       hipLaunchKernelGGL((gather_separable_mlp_kernel<T, O, INTERP, 16, true, 2>), dim3(nb),
                          dim3(kThreads), 0, stream, args, ty0, nsegs, bands_per_tile,
                          segs_per_tile, nwork);
-    else if (v == 6 && INTERP == XRS_INTERP_BILINEAR)
+    else if (v == 14) {
+      // LDS stage: 16-byte staging loads when every row start is 16-byte aligned
+      const int esz = (int)sizeof(T);
+      const bool vec = (16 % esz == 0) && ((uintptr_t)a.src % 16 == 0) &&
+                       ((a.src_sy * esz) % 16 == 0) && ((a.src_sn * esz) % 16 == 0) &&
+                       ((g.src_w * esz) % 16 == 0);
+      const char* cap_env = getenv("XRS_REPROJECT_LDS");
+      const int cap = cap_env ? atoi(cap_env) : 40 * 1024;
+      if (vec)
+        hipLaunchKernelGGL((gather_staged_kernel<T, O, INTERP, true>), dim3(nb), dim3(kThreads),
+                           (size_t)cap, stream, args, ty0, nsegs, bands_per_tile, segs_per_tile,
+                           nwork, cap);
+      else
+        hipLaunchKernelGGL((gather_staged_kernel<T, O, INTERP, false>), dim3(nb), dim3(kThreads),
+                           (size_t)cap, stream, args, ty0, nsegs, bands_per_tile, segs_per_tile,
+                           nwork, cap);
+    } else if (v == 6 && INTERP == XRS_INTERP_BILINEAR)
       hipLaunchKernelGGL((gather_bilinear_reuse_kernel<T, O, 4, true, false>), dim3(nb),
                          dim3(kThreads), 0, stream, args, ty0, nsegs, bands_per_tile,
                          segs_per_tile, nwork);
