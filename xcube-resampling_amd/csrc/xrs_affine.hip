@@ -433,8 +433,9 @@ affine_reduce_kernel(AffineArgs a, const AxisTab* __restrict__ ytab,
     // every element read from HBM once per tile with all of a wave's loads
     // issued before any is stored, instead of 4 dependent global taps per
     // sub-sample.  Tiles whose footprint exceeds the stage read globally.
-    const int r_lo = yb[2 * tj], r_hi = yb[2 * tj + 1];
-    const int c_lo = xb[2 * ti], c_hi = xb[2 * ti + 1];
+    const bool try_stage = stage_cap > 0;
+    const int r_lo = try_stage ? yb[2 * tj] : 0, r_hi = try_stage ? yb[2 * tj + 1] : -1;
+    const int c_lo = try_stage ? xb[2 * ti] : 0, c_hi = try_stage ? xb[2 * ti + 1] : -1;
     const int nr = r_hi - r_lo + 1, nc = c_hi - c_lo + 1;
     const int pitch = nc > 0 ? lds_pos(nc - 1) + 1 : 0;
     const bool staged = stage_cap > 0 && nr > 0 && nc > 0 && nr * pitch <= stage_cap &&
@@ -603,17 +604,18 @@ int launch(const AffineArgs& a, const AxisChunks& ay, const AxisChunks& ax, Axis
     const int64_t ntx = (a.out_w + kTileW - 1) / kTileW;
     const int64_t ntiles = ntx * nty * a.nt;
     const int nb = grid_blocks(ntiles, 1, 256 * 16);
-    // per tile row / column block: source span of its taps (for the LDS stage)
-    hipLaunchKernelGGL(affine_bounds_kernel, dim3(grid_blocks(nty + ntx, kThreads, 256)),
-                       dim3(kThreads), 0, st, ytab, xtab, ay.n, ax.n, kRedRows * a.dy,
-                       kTileW * a.dx, nty, ntx, yb, xb);
-    XRS_HIP_CHECK(hipGetLastError());
     // stage capacity from the scale (+ taps, mirror and rounding margin); the
     // kernel falls back to global taps for any tile whose span exceeds it
     const char* stage_knob = std::getenv("XRS_AFFINE_STAGE");
     // default off: staging without prefetch adds a dependent round trip per
     // tile (config 3: 1.89 ms staged vs 0.90 ms direct, MI355X)
     const bool use_stage = stage_knob && std::atoi(stage_knob) != 0;
+    if (use_stage) {  // per tile row / column block: source span of its taps
+      hipLaunchKernelGGL(affine_bounds_kernel, dim3(grid_blocks(nty + ntx, kThreads, 256)),
+                         dim3(kThreads), 0, st, ytab, xtab, ay.n, ax.n, kRedRows * a.dy,
+                         kTileW * a.dx, nty, ntx, yb, xb);
+      XRS_HIP_CHECK(hipGetLastError());
+    }
     const int64_t rows_need = (int64_t)ceil((kRedRows * a.dy - 1) * fabs(ay.scale)) + 3;
     const int64_t cols_need = (int64_t)ceil((kTileW * a.dx - 1) * fabs(ax.scale)) + 3;
     const int64_t cap = rows_need * (cols_need + (cols_need - 1) / 32 + 1);

@@ -81,6 +81,39 @@ __device__ inline int32_t next_box(const BBoxArgs& a, const double* bx, double x
   return INT32_MAX;
 }
 
+// Tile rows / columns whose closed interval [b[2t], b[2t+1]] contains v, for
+// interval arrays monotone in t (dir > 0: both ends non-decreasing, dir < 0:
+// non-increasing): a contiguous run found by two binary searches instead of a
+// scan over every tile (NaN -> empty).  Same inclusive compares as the scan.
+__device__ inline void monotone_hits(const double* b, int32_t n, double v, int dir,
+                                     int32_t& t0, int32_t& t1) {
+  int32_t lo = 0, hi = n;   // t0: first t with (dir > 0 ? b_hi >= v : b_lo <= v)
+  while (lo < hi) {
+    const int32_t m = (lo + hi) >> 1;
+    const bool ok = dir > 0 ? b[2 * m + 1] >= v : b[2 * m] <= v;
+    if (ok) hi = m; else lo = m + 1;
+  }
+  t0 = lo;
+  lo = 0; hi = n;           // t1 + 1: first t with !(dir > 0 ? b_lo <= v : b_hi >= v)
+  while (lo < hi) {
+    const int32_t m = (lo + hi) >> 1;
+    const bool ok = dir > 0 ? b[2 * m] <= v : b[2 * m + 1] >= v;
+    if (ok) lo = m + 1; else hi = m;
+  }
+  t1 = lo - 1;
+}
+
+// +1 / -1 if both interval ends are monotone non-decreasing / non-increasing
+// in t, else 0 (then the candidates are found by a full scan)
+__device__ inline int interval_dir(const double* b, int32_t n) {
+  bool inc = true, dec = true;
+  for (int32_t t = 1; t < n; ++t) {
+    inc = inc && b[2 * t] >= b[2 * t - 2] && b[2 * t + 1] >= b[2 * t - 1];
+    dec = dec && b[2 * t] <= b[2 * t - 2] && b[2 * t + 1] <= b[2 * t - 1];
+  }
+  return inc ? 1 : (dec ? -1 : 0);
+}
+
 // Each block owns one contiguous run of source pixels (spatially coherent:
 // few boxes per block).  SHARED: the box geometry and the per-box accumulators
 // live in LDS — the wave merges go to LDS atomics and each block flushes one
@@ -110,6 +143,8 @@ ij_bboxes_kernel(BBoxArgs a, int64_t chunk) {
   }
   const int64_t n = a.h * a.w;
   const int64_t p0 = (int64_t)blockIdx.x * chunk, p1 = min(n, p0 + chunk);
+  const int xdir = a.ntx > 0 ? interval_dir(bx, (int32_t)a.ntx) : 0;
+  const int ydir = a.ntx > 0 ? interval_dir(by, (int32_t)a.nty) : 0;
   // every lane of a wave iterates the same number of times (wave-uniform trip
   // count), so the wave-wide shuffles below always see all 64 lanes
   for (int64_t base = p0; base < p1; base += kThreads) {
@@ -125,10 +160,18 @@ ij_bboxes_kernel(BBoxArgs a, int64_t chunk) {
     }
     int32_t tx0 = 1, tx1 = 0, ty0 = 1, ty1 = 0;
     if (valid && a.ntx > 0) {  // x_min <= x <= x_max, y_min <= y <= y_max (bboxes.py:60-69)
-      for (int32_t t = 0; t < (int32_t)a.ntx; ++t)
-        if (bx[2 * t] <= x && x <= bx[2 * t + 1]) { if (tx0 > tx1) tx0 = t; tx1 = t; }
-      for (int32_t t = 0; t < (int32_t)a.nty; ++t)
-        if (by[2 * t] <= y && y <= by[2 * t + 1]) { if (ty0 > ty1) ty0 = t; ty1 = t; }
+      if (xdir != 0) {
+        monotone_hits(bx, (int32_t)a.ntx, x, xdir, tx0, tx1);
+      } else {
+        for (int32_t t = 0; t < (int32_t)a.ntx; ++t)
+          if (bx[2 * t] <= x && x <= bx[2 * t + 1]) { if (tx0 > tx1) tx0 = t; tx1 = t; }
+      }
+      if (ydir != 0) {
+        monotone_hits(by, (int32_t)a.nty, y, ydir, ty0, ty1);
+      } else {
+        for (int32_t t = 0; t < (int32_t)a.nty; ++t)
+          if (by[2 * t] <= y && y <= by[2 * t + 1]) { if (ty0 > ty1) ty0 = t; ty1 = t; }
+      }
     }
     int32_t cur = valid ? next_box(a, bx, x, y, tx0, tx1, ty0, ty1, -1) : INT32_MAX;
     while (true) {

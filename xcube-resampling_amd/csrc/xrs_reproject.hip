@@ -728,6 +728,10 @@ gather_staged_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t bands_per
 // item, 40 KB of LDS caps residency at 3 blocks/CU) = 7.9-11 ms for bands of
 // 6-16 rows vs 2.73 ms for 12 in the same run: kept for reference, a
 // double-buffered stage is the way to make it pay.
+// Also measured and dropped: the two horizontal taps as one dword-aligned
+// 8-byte load (global_load_dwordx2 at odd addresses): 4.08 ms vs 2.69 ms.
+// Reference point on the same box: nearest (1 tap) 2.08 ms = 6.4 TB/s, a
+// torch copy_ of the raster 2.8 ms — bilinear is tap-issue bound, not HBM.
 inline int variant() {
   const char* v = getenv("XRS_REPROJECT_VARIANT");
   return v ? atoi(v) : 12;
