@@ -227,16 +227,38 @@ int xrs_ij_bboxes(const double* x, const double* y, int64_t h, int64_t w, int64_
  *   swin, shin; float64 x_off, y_off} (row-major, ntiles_x per row): target
  *   tile origin/size, source window origin (si0 = -1: no source) and size,
  *   and the reference's per-tile dst_x/y_offset.
- * chunk_tile / chunk_q0 (device, nchunks): work list of 256-quad chunks.
+ * chunk_offsets (device, ntiles + 1): the work list of 256-quad chunks as
+ *   an exclusive prefix sum of each tile's chunk count (ceil((swin-1)*(shin-1)
+ *   / 256)); chunk_offsets[ntiles] = total.  Produced by xrs_rectify_tiles on
+ *   the device, so no host round trip is needed between K4 and K5.
+ * max_chunks: the total if the caller knows it (one chunk per block), else 0
+ *   (a persistent grid reads the total on the device).
  * x_scale = dst_x_res; y_scale = dst_y_res (j-axis up) or -dst_y_res.
  * keys: (dst_h, dst_w) uint32 scratch; ij: (2, dst_h, dst_w) float64 output
  *   (NaN where no quad hits).
  * ------------------------------------------------------------------------- */
 int xrs_rectify_ij(const double* x, const double* y, int64_t h, int64_t w, int64_t sy,
                    const void* tiles, int64_t ntiles, int64_t ntiles_x,
-                   const int64_t* chunk_tile, const int64_t* chunk_q0, int64_t nchunks,
+                   const int64_t* chunk_offsets, int64_t max_chunks,
                    int64_t dst_h, int64_t dst_w, double x_scale, double y_scale,
                    double uv_delta, uint32_t* keys, double* ij, void* stream);
+
+/* -------------------------------------------------------------------------
+ * xrs_rectify_tiles — the host-side tiling of _compute_target_source_ij
+ * (rectify.py:312-419: per target tile its source ij bbox, via
+ * ij_bboxes_from_xy_bboxes base.py:565-629 + bboxes.py:90-106, the source
+ * window it scans and the tile's dst_x/y offsets) done on the device from the
+ * raw K4 accumulators `acc` (xrs_ij_bboxes grid mode, ntiles_x*ntiles_y
+ * boxes), so K4 -> K5 needs no host synchronisation.
+ * tiles (device, ntiles records as in xrs_rectify_ij) and chunk_offsets
+ * (device, ntiles + 1) are written.  j_axis_up selects y_off = dst_y_min +
+ * r0*res (else dst_y_max - r0*res).
+ * ------------------------------------------------------------------------- */
+int xrs_rectify_tiles(const int32_t* acc, int64_t ntiles_x, int64_t ntiles_y, int64_t tile_w,
+                      int64_t tile_h, int64_t dst_w, int64_t dst_h, int64_t src_w,
+                      int64_t src_h, int64_t ij_border, double dst_x_min, double dst_y_min,
+                      double dst_y_max, double dst_x_res, double dst_y_res, int j_axis_up,
+                      void* tiles, int64_t* chunk_offsets, void* stream);
 
 /* -------------------------------------------------------------------------
  * xrs_rectify_var — replaces _compute_var_image_block / _sequential /

@@ -217,11 +217,19 @@ def config4(args):
                           args.steps, args.warmup)
         lines[interp] = k6_ms
 
-    def pipeline(interp):
-        t, n_x, _, _ = R.rectify_tiles(sgm, tgm, xy=xy)
-        ij_ = kernels.rectify_ij(xy[0], xy[1], t, n_x, tgm.height, tgm.width, tgm.x_res,
+    def pipeline(interp):   # K4 -> device tiling -> K5 -> K6, no host round trip
+        t = R._device_tiles(sgm, tgm, xy)
+        ij_ = kernels.rectify_ij(xy[0], xy[1], t, ntx, tgm.height, tgm.width, tgm.x_res,
                                  dst_y_scale, 1e-3)
         return kernels.rectify_var(ij_, src, interp, float("nan"))
+
+    # the device tiling reproduces the host tiling byte for byte
+    t_dev, offs = R._device_tiles(sgm, tgm, xy)
+    assert np.array_equal(t_dev.cpu().numpy(), tiles.view(np.uint8).ravel()), "device tiles"
+    assert torch.equal(torch.nan_to_num(pipeline("nearest"), 12345.0),
+                       torch.nan_to_num(kernels.rectify_var(ij, src, "nearest", float("nan")),
+                                        12345.0)), "device-tiled pipeline"
+
 
     npx = tgm.width * tgm.height
     S = w * h
@@ -246,7 +254,7 @@ def config4(args):
         cpu_v, px, dt = _cpu_loop(cpu_once, args.cpu_seconds, 0)
         _line(4, f"rectify {interp}: 4000x4800 jittered swath (f64 lon/lat, f32 var) -> "
                  f"{tgm.width}x{tgm.height} EPSG:4326 res 0.0027, 512^2 tiles "
-                 "(K4 bbox + host tiling + K5 + K6, end to end, coordinates resident in HBM)",
+                 "(K4 bbox + device tiling + K5 + K6, end to end, coordinates resident in HBM)",
               npx, ms, wall, 16 * S + 4 * S + 4 * npx,
               f"K5 rectify_claim+resolve {k5_ms:.3f} ms, K6 {lines[interp]:.3f} ms",
               dict(value=round(cpu_v, 2), unit="Mpixels/s", cores=cores, kind="port",

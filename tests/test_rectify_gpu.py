@@ -244,3 +244,42 @@ def test_resample_in_space_dispatches_rectify():
     tgm = xrs.GridMapping.regular((13, 13), (-0.25, 49.75), 0.5, "EPSG:4326")
     out = xrs.resample_in_space(dataset_2x2_irregular(), target_gm=tgm, interp_methods=0)
     np.testing.assert_almost_equal(out["rad"].values, RAD13)
+
+
+@pytest.mark.parametrize("j_up", [False, True])
+@pytest.mark.parametrize("tile", [(5, 7), (16, 16), (64, 32)])
+def test_device_tiling_matches_host_tiling(j_up, tile):
+    """xrs_rectify_tiles (K4 accumulators -> tile records + chunk offsets on the
+    device) reproduces the host tiling byte for byte, and K5 driven by it gives
+    the same ij image as K5 driven by host tiles."""
+    import torch
+
+    import xcube_resampling_amd as xrs
+    from xcube_resampling_amd import kernels
+    from xcube_resampling_amd import rectify as R
+
+    rng = np.random.default_rng(21)
+    h, w = 60, 50
+    jj, ii = np.mgrid[0:h, 0:w].astype(np.float64)
+    lon = 10.0 + 0.02 * ii + 0.004 * jj + rng.normal(0, 0.001, (h, w))
+    lat = 50.0 - 0.015 * jj + 0.003 * ii + rng.normal(0, 0.001, (h, w))
+    sgm = xrs.GridMapping.from_coords(xrs.DataArray(lon, ("y", "x"), name="lon"),
+                                      xrs.DataArray(lat, ("y", "x"), name="lat"), "EPSG:4326")
+    res = 0.012
+    x0, y0 = float(np.floor(lon.min() / res) * res), float(np.floor(lat.min() / res) * res)
+    size = (int(np.ceil((lon.max() - x0) / res)), int(np.ceil((lat.max() - y0) / res)))
+    tgm = xrs.GridMapping.regular(size, (x0, y0), res, "EPSG:4326", tile_size=tile,
+                                  is_j_axis_up=j_up)
+    xy = (torch.from_numpy(lon).cuda(), torch.from_numpy(lat).cuda())
+    tiles, ntx, _, _ = R.rectify_tiles(sgm, tgm, xy=xy)
+    t_dev, offs = R._device_tiles(sgm, tgm, xy)
+    assert np.array_equal(t_dev.cpu().numpy(), tiles.view(np.uint8).ravel())
+    nq = np.where(tiles["si0"] >= 0, np.maximum(tiles["swin"] - 1, 0).astype(np.int64)
+                  * np.maximum(tiles["shin"] - 1, 0), 0)
+    exp_offs = np.concatenate([[0], np.cumsum((nq + 255) // 256)])
+    np.testing.assert_array_equal(offs.cpu().numpy(), exp_offs)
+    ysc = tgm.y_res if j_up else -tgm.y_res
+    a = kernels.rectify_ij(xy[0], xy[1], tiles, ntx, tgm.height, tgm.width, tgm.x_res, ysc, 1e-3)
+    b = kernels.rectify_ij(xy[0], xy[1], (t_dev, offs), ntx, tgm.height, tgm.width, tgm.x_res,
+                           ysc, 1e-3)
+    assert_bitwise_equal(b.cpu().numpy(), a.cpu().numpy(), "device vs host tiles")

@@ -234,9 +234,7 @@ struct RectArgs {
   int64_t h, w, sy;
   const TileInfo* tiles;
   int64_t ntiles;
-  const int64_t* chunk_tile;   // work chunks: tile of chunk c
-  const int64_t* chunk_q0;     // first quad of chunk c (tile-local, raster order)
-  int64_t nchunks;
+  const int64_t* chunk_offs;   // (ntiles + 1): first 256-quad chunk of each tile
   int64_t dst_h, dst_w;
   double x_scale, y_scale;     // dst_x_res, dst_y_res (negated when j-axis down)
   double uv_delta;
@@ -304,14 +302,32 @@ __device__ inline int64_t pix_j(const RectArgs& a, const TileInfo& ti, double y)
 // their coordinates and target-pixel indices (two float64 divisions each)
 // come from the neighbour lane by a shuffle; only the last quad of a row or of
 // the wave loads/computes them itself.
+// Work list: chunk c belongs to the tile t with offs[t] <= c < offs[t+1] (the
+// offsets come from xrs_rectify_tiles on the device, or from the host); the
+// offsets are staged in LDS and searched per chunk.
+constexpr int kOffsLds = 2047;   // tiles whose offsets are copied to LDS (16 KB)
+
 template <bool PREREAD>
 __global__ void __launch_bounds__(kThreads)
 rectify_claim_kernel(RectArgs a) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  int64_t* offs_s = reinterpret_cast<int64_t*>(smem);
   const int lane = threadIdx.x & 63;
-  for (int64_t c = blockIdx.x; c < a.nchunks; c += gridDim.x) {
-    const TileInfo ti = a.tiles[a.chunk_tile[c]];
+  const bool lds_offs = a.ntiles <= kOffsLds;
+  if (lds_offs)
+    for (int64_t t = threadIdx.x; t <= a.ntiles; t += kThreads) offs_s[t] = a.chunk_offs[t];
+  __syncthreads();
+  const int64_t* offs = lds_offs ? offs_s : a.chunk_offs;
+  const int64_t nchunks = offs[a.ntiles];
+  for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+    int64_t lo = 0, hi = a.ntiles;   // last t with offs[t] <= c
+    while (hi - lo > 1) {
+      const int64_t m = (lo + hi) >> 1;
+      if (offs[m] <= c) lo = m; else hi = m;
+    }
+    const TileInfo ti = a.tiles[lo];
     const int64_t nq_i = ti.swin - 1;
-    const int64_t q = a.chunk_q0[c] + threadIdx.x;
+    const int64_t q = (c - offs[lo]) * kThreads + threadIdx.x;
     const bool valid = ti.si0 >= 0 && nq_i > 0 && q < nq_i * (int64_t)(ti.shin - 1);
     int64_t lj = 0, li = 0, qj = 0, qi = 0;
     Quad Q{NAN, NAN, NAN, NAN, NAN, NAN, NAN, NAN};
@@ -452,8 +468,95 @@ rectify_var_kernel(const double* __restrict__ ij, int64_t dst_h, int64_t dst_w,
   }
 }
 
+// ---- per-tile records + chunk offsets from the K4 accumulators ---------------
+// Mirrors the host tiling (rectify.py:312-419 via base.py:565-629 and
+// bboxes.py:90-106): ij bbox = [min i, min j, max i + 1, max j + 1] widened by
+// ij_border and clipped, source window = [i_min, min(i_max + 1, w)), target
+// offsets dst_x_min + c0 * res (python float arithmetic, no contraction).
+// One block: records in parallel, then an exclusive scan of the per-tile
+// 256-quad chunk counts.
+__global__ void __launch_bounds__(kThreads)
+rectify_tiles_kernel(const int32_t* __restrict__ acc, int64_t ntx, int64_t nty, int64_t tw,
+                     int64_t th, int64_t dst_w, int64_t dst_h, int64_t src_w, int64_t src_h,
+                     int64_t ij_border, double x_min, double y_min, double y_max,
+                     double x_res, double y_res, int j_up, TileInfo* __restrict__ tiles,
+                     int64_t* __restrict__ offs) {
+  __shared__ int64_t part[kThreads];
+  const int64_t n = ntx * nty;
+  int64_t carry = 0;
+  for (int64_t base = 0; base < n; base += kThreads) {
+    const int64_t t = base + threadIdx.x;
+    int64_t nch = 0;
+    if (t < n) {
+      const int64_t ty = t / ntx, tx = t - ty * ntx;
+      TileInfo ti;
+      ti.r0 = (int32_t)(ty * th);
+      ti.c0 = (int32_t)(tx * tw);
+      ti.th = (int32_t)min(th, dst_h - ty * th);
+      ti.tw = (int32_t)min(tw, dst_w - tx * tw);
+      int64_t i0 = -1, j0 = -1, i1 = -1, j1 = -1;
+      if (acc[4 * t + 2] >= 0) {
+        i0 = acc[4 * t + 0]; j0 = acc[4 * t + 1];
+        i1 = (int64_t)acc[4 * t + 2] + 1; j1 = (int64_t)acc[4 * t + 3] + 1;
+        if (ij_border != 0) {
+          i0 = max(i0 - ij_border, (int64_t)0);
+          j0 = max(j0 - ij_border, (int64_t)0);
+          i1 = min(i1 + ij_border, src_w);
+          j1 = min(j1 + ij_border, src_h);
+        }
+      }
+      const bool none = i0 == -1;
+      ti.si0 = (int32_t)(none ? -1 : i0);
+      ti.sj0 = (int32_t)(none ? -1 : j0);
+      ti.swin = (int32_t)(none ? 0 : min(i1 + 1, src_w) - i0);
+      ti.shin = (int32_t)(none ? 0 : min(j1 + 1, src_h) - j0);
+      ti.x_off = x_min + (double)ti.c0 * x_res;
+      ti.y_off = j_up ? y_min + (double)ti.r0 * y_res : y_max - (double)ti.r0 * y_res;
+      tiles[t] = ti;
+      const int64_t nq = none ? 0 : max((int64_t)ti.swin - 1, (int64_t)0) *
+                                        max((int64_t)ti.shin - 1, (int64_t)0);
+      nch = (nq + kThreads - 1) / kThreads;
+    }
+    // inclusive scan of nch over the block (Hillis-Steele in LDS)
+    part[threadIdx.x] = nch;
+    __syncthreads();
+    for (int o = 1; o < kThreads; o <<= 1) {
+      const int64_t v = threadIdx.x >= (unsigned)o ? part[threadIdx.x - o] : 0;
+      __syncthreads();
+      part[threadIdx.x] += v;
+      __syncthreads();
+    }
+    if (t < n) offs[t] = carry + part[threadIdx.x] - nch;
+    carry += part[kThreads - 1];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) offs[n] = carry;
+}
+
 }  // namespace
 }  // namespace xrs
+
+extern "C" int xrs_rectify_tiles(const int32_t* acc, int64_t ntiles_x, int64_t ntiles_y,
+                                 int64_t tile_w, int64_t tile_h, int64_t dst_w, int64_t dst_h,
+                                 int64_t src_w, int64_t src_h, int64_t ij_border,
+                                 double dst_x_min, double dst_y_min, double dst_y_max,
+                                 double dst_x_res, double dst_y_res, int j_axis_up, void* tiles,
+                                 int64_t* chunk_offsets, void* stream) {
+  using namespace xrs;
+  if (!acc || !tiles || !chunk_offsets || ntiles_x < 1 || ntiles_y < 1 || tile_w < 1 ||
+      tile_h < 1 || dst_w < 1 || dst_h < 1 || src_w < 1 || src_h < 1 || ij_border < 0 ||
+      (ntiles_x - 1) * tile_w >= dst_w || (ntiles_y - 1) * tile_h >= dst_h) {
+    xrs_set_error("xrs_rectify_tiles: invalid argument");
+    return XRS_ERR_ARG;
+  }
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(rectify_tiles_kernel, dim3(1), dim3(kThreads), 0, st, acc, ntiles_x,
+                     ntiles_y, tile_w, tile_h, dst_w, dst_h, src_w, src_h, ij_border, dst_x_min,
+                     dst_y_min, dst_y_max, dst_x_res, dst_y_res, j_axis_up,
+                     static_cast<TileInfo*>(tiles), chunk_offsets);
+  XRS_HIP_CHECK(hipGetLastError());
+  return XRS_OK;
+}
 
 extern "C" int xrs_ij_bboxes(const double* x, const double* y, int64_t h, int64_t w,
                              int64_t sy, int64_t nboxes, int64_t ntx, int64_t nty,
@@ -481,27 +584,28 @@ extern "C" int xrs_ij_bboxes(const double* x, const double* y, int64_t h, int64_
 
 extern "C" int xrs_rectify_ij(const double* x, const double* y, int64_t h, int64_t w,
                               int64_t sy, const void* tiles, int64_t ntiles, int64_t ntiles_x,
-                              const int64_t* chunk_tile, const int64_t* chunk_q0,
-                              int64_t nchunks, int64_t dst_h, int64_t dst_w, double x_scale,
+                              const int64_t* chunk_offsets, int64_t max_chunks,
+                              int64_t dst_h, int64_t dst_w, double x_scale,
                               double y_scale, double uv_delta, uint32_t* keys, double* ij,
                               void* stream) {
   using namespace xrs;
   if (!x || !y || !tiles || !keys || !ij || h < 2 || w < 2 || sy < w || ntiles < 1 ||
-      dst_h < 1 || dst_w < 1 || h * w >= (int64_t)UINT32_MAX || (nchunks > 0 && (!chunk_tile || !chunk_q0))) {
+      dst_h < 1 || dst_w < 1 || h * w >= (int64_t)UINT32_MAX || !chunk_offsets || max_chunks < 0) {
     xrs_set_error("xrs_rectify_ij: invalid argument");
     return XRS_ERR_ARG;
   }
   RectArgs a;
   a.x = x; a.y = y; a.h = h; a.w = w; a.sy = sy;
   a.tiles = static_cast<const TileInfo*>(tiles); a.ntiles = ntiles;
-  a.chunk_tile = chunk_tile; a.chunk_q0 = chunk_q0; a.nchunks = nchunks;
+  a.chunk_offs = chunk_offsets;
   a.dst_h = dst_h; a.dst_w = dst_w; a.x_scale = x_scale; a.y_scale = y_scale;
   a.uv_delta = uv_delta; a.keys = keys; a.ij = ij;
   hipStream_t st = static_cast<hipStream_t>(stream);
   XRS_HIP_CHECK(hipMemsetAsync(keys, 0xFF, (size_t)(dst_h * dst_w) * sizeof(uint32_t), st));
-  if (nchunks > 0) {
+  {
     // A/B knobs: XRS_RECTIFY_PREREAD (skip quads whose pixel is already
-    // claimed by a smaller key), XRS_RECTIFY_BLOCKS_PER_CU (0 = one chunk per block)
+    // claimed by a smaller key), XRS_RECTIFY_BLOCKS_PER_CU (0 = one chunk per
+    // block when the caller knows the chunk count, else 16 blocks per CU)
     const char* pr = getenv("XRS_RECTIFY_PREREAD");
     const char* bpc = getenv("XRS_RECTIFY_BLOCKS_PER_CU");
     // measured (config 4): no pre-read 2.04 ms vs 3.42 ms (the dependent read
@@ -509,11 +613,13 @@ extern "C" int xrs_rectify_ij(const double* x, const double* y, int64_t h, int64
     // one chunk per block 1.98 vs 2.04 ms
     const bool preread = pr ? atoi(pr) != 0 : false;
     const int cap = bpc && atoi(bpc) > 0 ? 256 * atoi(bpc) : (1 << 24);
-    const int nb = grid_blocks(nchunks, 1, cap);
+    const int nb = max_chunks > 0 ? grid_blocks(max_chunks, 1, cap)
+                                  : grid_blocks(256 * 16, 1, cap);
+    const size_t lds = ntiles <= kOffsLds ? (size_t)(ntiles + 1) * sizeof(int64_t) : 0;
     if (preread)
-      hipLaunchKernelGGL(rectify_claim_kernel<true>, dim3(nb), dim3(kThreads), 0, st, a);
+      hipLaunchKernelGGL(rectify_claim_kernel<true>, dim3(nb), dim3(kThreads), lds, st, a);
     else
-      hipLaunchKernelGGL(rectify_claim_kernel<false>, dim3(nb), dim3(kThreads), 0, st, a);
+      hipLaunchKernelGGL(rectify_claim_kernel<false>, dim3(nb), dim3(kThreads), lds, st, a);
     XRS_HIP_CHECK(hipGetLastError());
   }
   const int nb2 = grid_blocks(dst_h * dst_w, kThreads, 256 * 8);

@@ -106,16 +106,9 @@ TILE_INFO_DTYPE = np.dtype([("r0", np.int32), ("c0", np.int32), ("th", np.int32)
                             ("y_off", np.float64)])
 
 
-def ij_bboxes(x_image, y_image, xy_bboxes, xy_border: float = 0.0, ij_border: int = 0,
-              grid: tuple[int, int] | None = None, device=None, stream=None) -> np.ndarray:
-    """K4 — gridmapping/bboxes.py:28-106 (compute_ij_bboxes) on the device.
-
-    x_image, y_image: (h, w) source coordinates (numpy or device tensors).
-    grid: (ntx, nty) when the boxes are the tiles of a regular grid (box k =
-    ty*ntx + tx); enables the per-pixel candidate search over tile columns and
-    rows instead of testing every box.
-    Returns the (n, 4) int64 ij bboxes [i_min, j_min, i_max, j_max] (-1 = none).
-    """
+def _ij_bboxes_launch(x_image, y_image, xy_bboxes, xy_border, grid, device, stream):
+    """Launch K4; returns (device int32 accumulators (n, 4), n, (w, h), grid
+    mode used)."""
     device = require_device(device if device is not None else getattr(x_image, "device", None))
     x = to_device(x_image, device, np.float64)
     y = to_device(y_image, device, np.float64)
@@ -143,6 +136,21 @@ def ij_bboxes(x_image, y_image, xy_bboxes, xy_border: float = 0.0, ij_border: in
     rc = _native.lib().xrs_ij_bboxes(ptr(x), ptr(y), h, w, x.stride(0), n, ntx, nty, ptr(bx),
                                      ptr(by), ptr(acc), stream_handle(device, stream))
     _native.check(rc, "xrs_ij_bboxes")
+    return acc, n, (w, h), ntx > 0
+
+
+def ij_bboxes(x_image, y_image, xy_bboxes, xy_border: float = 0.0, ij_border: int = 0,
+              grid: tuple[int, int] | None = None, device=None, stream=None) -> np.ndarray:
+    """K4 — gridmapping/bboxes.py:28-106 (compute_ij_bboxes) on the device.
+
+    x_image, y_image: (h, w) source coordinates (numpy or device tensors).
+    grid: (ntx, nty) when the boxes are the tiles of a regular grid (box k =
+    ty*ntx + tx); enables the per-pixel candidate search over tile columns and
+    rows instead of testing every box.
+    Returns the (n, 4) int64 ij bboxes [i_min, j_min, i_max, j_max] (-1 = none).
+    """
+    acc, n, (w, h), _ = _ij_bboxes_launch(x_image, y_image, xy_bboxes, xy_border, grid, device,
+                                          stream)
     acc = acc.cpu().numpy().astype(np.int64)
     out = np.full((n, 4), -1, dtype=np.int64)
     found = acc[:, 2] >= 0
@@ -157,34 +165,62 @@ def ij_bboxes(x_image, y_image, xy_bboxes, xy_border: float = 0.0, ij_border: in
     return out
 
 
+def rectify_tiles_device(x_image, y_image, target_xy_bboxes, xy_border: float, ij_border: int,
+                         grid: tuple[int, int], tile_size: tuple[int, int],
+                         dst_size: tuple[int, int], dst_xy_min_max: tuple, dst_res: tuple,
+                         j_axis_up: bool, device=None, stream=None):
+    """K4 + xrs_rectify_tiles: the per-tile records and chunk offsets of
+    rectify.py:312-419 computed and left on the device (no host round trip).
+    Returns (tiles uint8 tensor of TILE_INFO records, chunk offsets int64
+    tensor), or None when the boxes are not a regular tile grid."""
+    acc, n, (w, h), is_grid = _ij_bboxes_launch(x_image, y_image, target_xy_bboxes, xy_border,
+                                                grid, device, stream)
+    if not is_grid:
+        return None
+    device = acc.device
+    ntx, nty = grid
+    tiles = torch().empty(n * TILE_INFO_DTYPE.itemsize, dtype=torch().uint8, device=device)
+    offs = torch().empty(n + 1, dtype=torch().int64, device=device)
+    x_min, y_min, y_max = dst_xy_min_max
+    rc = _native.lib().xrs_rectify_tiles(
+        ptr(acc), ntx, nty, tile_size[0], tile_size[1], dst_size[0], dst_size[1], w, h,
+        int(ij_border), float(x_min), float(y_min), float(y_max), float(dst_res[0]),
+        float(dst_res[1]), int(bool(j_axis_up)), ptr(tiles), ptr(offs),
+        stream_handle(device, stream))
+    _native.check(rc, "xrs_rectify_tiles")
+    return tiles, offs
+
+
 def rectify_ij(x_image, y_image, tiles: np.ndarray, ntiles_x: int, dst_h: int, dst_w: int,
                x_scale: float, y_scale: float, uv_delta: float, device=None, stream=None):
     """K5 — per target pixel the fractional source (i, j) (rectify.py:373-576).
 
-    tiles: structured array of TILE_INFO_DTYPE (row-major tile order).
+    tiles: structured array of TILE_INFO_DTYPE (row-major tile order), or
+    the (tiles, chunk offsets) device pair of rectify_tiles_device.
     Returns a device tensor (2, dst_h, dst_w) float64 (NaN = no source pixel).
     """
     device = require_device(device)
     x = to_device(x_image, device, np.float64)
     y = to_device(y_image, device, np.float64)
     h, w = x.shape
-    tiles = np.ascontiguousarray(tiles, dtype=TILE_INFO_DTYPE)
-    nq = np.where(tiles["si0"] >= 0,
-                  np.maximum(tiles["swin"].astype(np.int64) - 1, 0)
-                  * np.maximum(tiles["shin"].astype(np.int64) - 1, 0), 0)
-    per = 256
-    nch = (nq + per - 1) // per
-    chunk_tile = np.repeat(np.arange(len(tiles), dtype=np.int64), nch)
-    chunk_q0 = (np.concatenate([np.arange(k, dtype=np.int64) for k in nch]) * per
-                if len(nch) else np.zeros(0, np.int64))
-    t_dev = torch().from_numpy(tiles.view(np.uint8).copy()).to(device)
-    ct = to_device(chunk_tile if chunk_tile.size else np.zeros(1, np.int64), device)
-    cq = to_device(chunk_q0 if chunk_q0.size else np.zeros(1, np.int64), device)
+    if isinstance(tiles, np.ndarray):   # host tiles: offsets computed here
+        tiles = np.ascontiguousarray(tiles, dtype=TILE_INFO_DTYPE)
+        nq = np.where(tiles["si0"] >= 0,
+                      np.maximum(tiles["swin"].astype(np.int64) - 1, 0)
+                      * np.maximum(tiles["shin"].astype(np.int64) - 1, 0), 0)
+        nch = (nq + 255) // 256
+        offs_h = np.concatenate([[0], np.cumsum(nch)]).astype(np.int64)
+        ntiles, max_chunks = len(tiles), int(offs_h[-1])
+        t_dev = torch().from_numpy(tiles.view(np.uint8).copy()).to(device)
+        offs = to_device(offs_h, device)
+    else:                                 # device tiles from rectify_tiles_device
+        t_dev, offs = tiles
+        ntiles, max_chunks = offs.numel() - 1, 0
     keys = torch().empty((dst_h, dst_w), dtype=torch().int32, device=device)
     ij = torch().empty((2, dst_h, dst_w), dtype=torch().float64, device=device)
-    rc = _native.lib().xrs_rectify_ij(ptr(x), ptr(y), h, w, x.stride(0), ptr(t_dev), len(tiles),
-                                      ntiles_x, ptr(ct), ptr(cq), int(chunk_tile.size), dst_h,
-                                      dst_w, float(x_scale), float(y_scale), float(uv_delta),
+    rc = _native.lib().xrs_rectify_ij(ptr(x), ptr(y), h, w, x.stride(0), ptr(t_dev), ntiles,
+                                      ntiles_x, ptr(offs), max_chunks, dst_h, dst_w,
+                                      float(x_scale), float(y_scale), float(uv_delta),
                                       ptr(keys), ptr(ij), stream_handle(device, stream))
     _native.check(rc, "xrs_rectify_ij")
     return ij

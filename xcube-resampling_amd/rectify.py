@@ -165,10 +165,29 @@ def _compute_target_source_ij(source_gm: GridMapping, target_gm: GridMapping,
     device = require_device()
     xy = source_gm.xy_coords.data
     xy = (to_device(xy[0], device, np.float64), to_device(xy[1], device, np.float64))
-    tiles, ntx, _, _ = rectify_tiles(source_gm, target_gm, uv_delta, xy=xy)
     dst_y_scale = target_gm.y_res if target_gm.is_j_axis_up else -target_gm.y_res
+    tiles = _device_tiles(source_gm, target_gm, xy)
+    if tiles is None:   # boxes not a regular tile grid: host tiling
+        tiles, ntx, _, _ = rectify_tiles(source_gm, target_gm, uv_delta, xy=xy)
+    else:
+        ntx = len(chunk_sizes(target_gm.width, target_gm.tile_width))
     return kernels.rectify_ij(xy[0], xy[1], tiles, ntx, target_gm.height, target_gm.width,
                               target_gm.x_res, dst_y_scale, uv_delta)
+
+
+def _device_tiles(source_gm: GridMapping, target_gm: GridMapping, xy):
+    """rectify_tiles with K4's accumulators turned into tile records and chunk
+    offsets on the device (xrs_rectify_tiles): no host synchronisation
+    between K4 and K5."""
+    dst_w, dst_h = target_gm.width, target_gm.height
+    tw, th = target_gm.tile_width, target_gm.tile_height
+    dst_x_min, dst_y_min, dst_x_max, dst_y_max = target_gm.xy_bbox
+    xy_border = min(min(2 * (dst_w / tw) * target_gm.x_res, 2 * (dst_h / th) * target_gm.y_res),
+                    min(0.5 * (dst_x_max - dst_x_min), 0.5 * (dst_y_max - dst_y_min)))
+    grid = (len(chunk_sizes(dst_w, tw)), len(chunk_sizes(dst_h, th)))
+    return kernels.rectify_tiles_device(
+        xy[0], xy[1], target_gm.xy_bboxes, xy_border, 1, grid, (tw, th), (dst_w, dst_h),
+        (dst_x_min, dst_y_min, dst_y_max), target_gm.xy_res, target_gm.is_j_axis_up)
 
 
 def _rectify_data_array(data_array: DataArray, var_name, target_gm: GridMapping,
