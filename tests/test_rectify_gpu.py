@@ -283,3 +283,40 @@ def test_device_tiling_matches_host_tiling(j_up, tile):
     b = kernels.rectify_ij(xy[0], xy[1], (t_dev, offs), ntx, tgm.height, tgm.width, tgm.x_res,
                            ysc, 1e-3)
     assert_bitwise_equal(b.cpu().numpy(), a.cpu().numpy(), "device vs host tiles")
+
+
+def test_claim_fast_decisions_equal_exact_divisions(monkeypatch):
+    """K5a decides pixel windows and triangle hits by reciprocal
+    multiplication with an exact-division fallback near every boundary; forcing
+    the exact path everywhere (XRS_RECTIFY_EXACT=1) gives the same ij image on
+    a jittered swath with degenerate (duplicate) and NaN coordinates."""
+    import torch
+
+    import xcube_resampling_amd as xrs
+    from xcube_resampling_amd import kernels
+    from xcube_resampling_amd import rectify as R
+
+    rng = np.random.default_rng(5)
+    h, w = 120, 90
+    jj, ii = np.mgrid[0:h, 0:w].astype(np.float64)
+    lon = 3.0 + 0.01 * ii + 0.002 * jj + rng.normal(0, 0.002, (h, w))
+    lat = 40.0 - 0.008 * jj + 0.001 * ii + rng.normal(0, 0.002, (h, w))
+    lon[10, 10:14] = lon[10, 10]                  # degenerate quads
+    lat[50:52, 30] = np.nan                       # missing coordinates
+    lon[70, 5] = lon[70, 4]
+    sgm = xrs.GridMapping.from_coords(xrs.DataArray(lon, ("y", "x"), name="lon"),
+                                      xrs.DataArray(lat, ("y", "x"), name="lat"), "EPSG:4326")
+    res = 0.005
+    x0 = float(np.floor(np.nanmin(lon) / res) * res)
+    y0 = float(np.floor(np.nanmin(lat) / res) * res)
+    size = (int(np.ceil((np.nanmax(lon) - x0) / res)), int(np.ceil((np.nanmax(lat) - y0) / res)))
+    tgm = xrs.GridMapping.regular(size, (x0, y0), res, "EPSG:4326", tile_size=(48, 40))
+    xy = (torch.from_numpy(lon).cuda(), torch.from_numpy(lat).cuda())
+    tiles, ntx, _, _ = R.rectify_tiles(sgm, tgm, xy=xy)
+    run = lambda: kernels.rectify_ij(xy[0], xy[1], tiles, ntx, tgm.height, tgm.width,  # noqa
+                                     tgm.x_res, -tgm.y_res, 1e-3).cpu().numpy()
+    fast = run()
+    monkeypatch.setenv("XRS_RECTIFY_EXACT", "1")
+    exact = run()
+    assert_bitwise_equal(fast, exact, "fast vs exact decisions")
+    assert np.isfinite(fast).sum() > 0.5 * fast.size

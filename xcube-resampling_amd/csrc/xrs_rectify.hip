@@ -238,6 +238,8 @@ struct RectArgs {
   int64_t dst_h, dst_w;
   double x_scale, y_scale;     // dst_x_res, dst_y_res (negated when j-axis down)
   double uv_delta;
+  double inv_x, inv_y;         // 1 / x_scale, 1 / y_scale (claim fast paths)
+  double margin;               // relative decision margin (inf: always exact)
   uint32_t* keys;              // (dst_h, dst_w) claim keys, 0xFFFFFFFF = free
   double* ij;                  // (2, dst_h, dst_w) output
 };
@@ -296,6 +298,41 @@ __device__ inline int64_t pix_j(const RectArgs& a, const TileInfo& ti, double y)
   return f64_to_i64_x86(floor((y - ti.y_off) / a.y_scale));
 }
 
+// ---- division-free decisions with an exact fallback (K5a) ---------------------
+// K5a only needs the integer pixel window of each corner and the hit / no-hit
+// decision of each triangle.  Both are taken from a multiplication by the
+// reciprocal (error <= a few ulps) whenever the value is clearly (relative
+// margin 1e-9) away from the decision boundary — an integer for floor, the
+// uv limits for a hit — and from the reference's exact divisions otherwise,
+// so every decision equals the reference's (NaN / inf always take the exact
+// path).  K5b recomputes the winner with the exact divisions.
+constexpr double kMargin = 1e-9;
+
+__device__ inline int64_t pix_fast(double x, double off, double scale, double inv,
+                                   double margin) {
+  const double d = x - off;
+  const double q = d * inv;
+  const double fq = floor(q);
+  const double m = margin * (1.0 + fabs(q));
+  if (q - fq > m && (fq + 1.0) - q > m) return f64_to_i64_x86(fq);
+  return f64_to_i64_x86(floor(d / scale));
+}
+
+// triangle test of rectify.py:556-573 (u from fu over the (p0, p2) edge, v
+// from fv over (p0, p1)), decided as above; r = 1 / det
+__device__ inline bool tri_hit_fast(double dx, double dy, double ox, double oy, double ux,
+                                    double uy, double vx, double vy, double det, double r,
+                                    double umin, double uvmax, double margin) {
+  if (det == 0.0) return false;
+  const double nu = fu(dx, dy, ox, oy, ux, uy), nv = fv(dx, dy, ox, oy, vx, vy);
+  const double u = nu * r, v = nv * r, s = u + v;
+  if (fabs(u - umin) > margin * (1.0 + fabs(u)) && fabs(v - umin) > margin * (1.0 + fabs(v)) &&
+      fabs(s - uvmax) > margin * (1.0 + fabs(s)))
+    return u >= umin && v >= umin && s <= uvmax;
+  const double ue = nu / det, ve = nv / det;
+  return ue >= umin && ve >= umin && ue + ve <= uvmax;
+}
+
 // ---- K5a: claim target pixels with the raster-order key of hitting quads -------
 // Lanes take consecutive quads of a window row: the right-hand corners (p1,
 // p3) of a quad are the left-hand corners (p0, p2) of the next lane's quad, so
@@ -340,8 +377,8 @@ rectify_claim_kernel(RectArgs a) {
       const int64_t r0 = qj * a.sy, r1 = (qj + 1) * a.sy;
       Q.x0 = a.x[r0 + qi]; Q.y0 = a.y[r0 + qi];
       Q.x2 = a.x[r1 + qi]; Q.y2 = a.y[r1 + qi];
-      pi0 = pix_i(a, ti, Q.x0); pj0 = pix_j(a, ti, Q.y0);
-      pi2 = pix_i(a, ti, Q.x2); pj2 = pix_j(a, ti, Q.y2);
+      pi0 = pix_fast(Q.x0, ti.x_off, a.x_scale, a.inv_x, a.margin); pj0 = pix_fast(Q.y0, ti.y_off, a.y_scale, a.inv_y, a.margin);
+      pi2 = pix_fast(Q.x2, ti.x_off, a.x_scale, a.inv_x, a.margin); pj2 = pix_fast(Q.y2, ti.y_off, a.y_scale, a.inv_y, a.margin);
     }
     // right-hand corners from the next lane (all lanes take part in shuffles)
     Q.x1 = __shfl_down(Q.x0, 1, 64); Q.y1 = __shfl_down(Q.y0, 1, 64);
@@ -353,8 +390,8 @@ rectify_claim_kernel(RectArgs a) {
       const int64_t r0 = qj * a.sy, r1 = (qj + 1) * a.sy;
       Q.x1 = a.x[r0 + qi + 1]; Q.y1 = a.y[r0 + qi + 1];
       Q.x3 = a.x[r1 + qi + 1]; Q.y3 = a.y[r1 + qi + 1];
-      pi1 = pix_i(a, ti, Q.x1); pj1 = pix_j(a, ti, Q.y1);
-      pi3 = pix_i(a, ti, Q.x3); pj3 = pix_j(a, ti, Q.y3);
+      pi1 = pix_fast(Q.x1, ti.x_off, a.x_scale, a.inv_x, a.margin); pj1 = pix_fast(Q.y1, ti.y_off, a.y_scale, a.inv_y, a.margin);
+      pi3 = pix_fast(Q.x3, ti.x_off, a.x_scale, a.inv_x, a.margin); pj3 = pix_fast(Q.y3, ti.y_off, a.y_scale, a.inv_y, a.margin);
     }
     int64_t imin = min(min(pi0, pi1), min(pi2, pi3)), imax = max(max(pi0, pi1), max(pi2, pi3));
     int64_t jmin = min(min(pj0, pj1), min(pj2, pj3)), jmax = max(max(pj0, pj1), max(pj2, pj3));
@@ -364,6 +401,8 @@ rectify_claim_kernel(RectArgs a) {
     double det_a, det_b;
     quad_dets(Q, det_a, det_b);
     if (det_a == 0.0 && det_b == 0.0) continue;
+    const double ra = det_a != 0.0 ? 1.0 / det_a : 0.0, rb = det_b != 0.0 ? 1.0 / det_b : 0.0;
+    const double umin = -a.uv_delta, uvmax = 1.0 + 2 * a.uv_delta;
     const uint32_t key = (uint32_t)(qj * a.w + qi);
     for (int64_t dj = jmin; dj <= jmax; ++dj) {
       const double dy = ti.y_off + ((double)dj + 0.5) * a.y_scale;
@@ -371,8 +410,10 @@ rectify_claim_kernel(RectArgs a) {
       for (int64_t di = imin; di <= imax; ++di) {
         if (PREREAD && krow[di] <= key) continue;  // already claimed by an earlier quad
         const double dx = ti.x_off + ((double)di + 0.5) * a.x_scale;
-        double cu, cv;
-        if (quad_hit(a, Q, dx, dy, det_a, det_b, cu, cv)) atomicMin(&krow[di], key);
+        const bool hit =
+            tri_hit_fast(dx, dy, Q.x0, Q.y0, Q.x2, Q.y2, Q.x1, Q.y1, det_a, ra, umin, uvmax, a.margin) ||
+            tri_hit_fast(dx, dy, Q.x3, Q.y3, Q.x1, Q.y1, Q.x2, Q.y2, det_b, rb, umin, uvmax, a.margin);
+        if (hit) atomicMin(&krow[di], key);
       }
     }
   }
@@ -600,6 +641,10 @@ extern "C" int xrs_rectify_ij(const double* x, const double* y, int64_t h, int64
   a.chunk_offs = chunk_offsets;
   a.dst_h = dst_h; a.dst_w = dst_w; a.x_scale = x_scale; a.y_scale = y_scale;
   a.uv_delta = uv_delta; a.keys = keys; a.ij = ij;
+  a.inv_x = 1.0 / x_scale; a.inv_y = 1.0 / y_scale;
+  // A/B + test knob: XRS_RECTIFY_EXACT=1 takes the exact divisions everywhere
+  const char* ex = getenv("XRS_RECTIFY_EXACT");
+  a.margin = ex && atoi(ex) != 0 ? INFINITY : kMargin;
   hipStream_t st = static_cast<hipStream_t>(stream);
   XRS_HIP_CHECK(hipMemsetAsync(keys, 0xFF, (size_t)(dst_h * dst_w) * sizeof(uint32_t), st));
   {
