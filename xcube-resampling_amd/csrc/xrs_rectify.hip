@@ -326,36 +326,50 @@ __device__ inline bool tri_hit_fast(double dx, double dy, double ox, double oy, 
   if (det == 0.0) return false;
   const double nu = fu(dx, dy, ox, oy, ux, uy), nv = fv(dx, dy, ox, oy, vx, vy);
   const double u = nu * r, v = nv * r, s = u + v;
-  if (fabs(u - umin) > margin * (1.0 + fabs(u)) && fabs(v - umin) > margin * (1.0 + fabs(v)) &&
-      fabs(s - uvmax) > margin * (1.0 + fabs(s)))
+  // |u - nu/det| <= ~3 ulp(u): below 1e-9 for |u| < 1e5, and beyond that u is
+  // farther than its error from every limit — an absolute margin suffices
+  if (fabs(u - umin) > margin && fabs(v - umin) > margin && fabs(s - uvmax) > margin)
     return u >= umin && v >= umin && s <= uvmax;
   const double ue = nu / det, ve = nv / det;
   return ue >= umin && ve >= umin && ue + ve <= uvmax;
 }
 
 // ---- K5a: claim target pixels with the raster-order key of hitting quads -------
-// Lanes take consecutive quads of a window row: the right-hand corners (p1,
-// p3) of a quad are the left-hand corners (p0, p2) of the next lane's quad, so
-// their coordinates and target-pixel indices (two float64 divisions each)
-// come from the neighbour lane by a shuffle; only the last quad of a row or of
-// the wave loads/computes them itself.
+// Phase 1, one quad per lane: lanes take consecutive quads of a window row, so
+// the right-hand corners (p1, p3) of a quad are the left-hand corners (p0, p2)
+// of the next lane's quad and come from it by a shuffle (only the last quad of
+// a row or of the wave loads them itself); the quad's clipped target-pixel
+// window and determinants are parked in LDS.
+// Phase 2, load-balanced: the wave's (quad, window pixel) tests are numbered by
+// a wave prefix sum of the window sizes and dealt round-robin to the 64 lanes
+// — every lane runs ceil(total / 64) tests instead of the wave running the
+// largest window of any lane (quads culled by the tile or degenerate cost
+// nothing), each test reading its quad from LDS.
 // Work list: chunk c belongs to the tile t with offs[t] <= c < offs[t+1] (the
 // offsets come from xrs_rectify_tiles on the device, or from the host); the
 // offsets are staged in LDS and searched per chunk.
 constexpr int kOffsLds = 2047;   // tiles whose offsets are copied to LDS (16 KB)
+constexpr int kQd = 12;          // doubles per staged quad: 8 corners, det_a/b, 1/det_a/b
 
-template <bool PREREAD>
+struct ClaimLds {
+  double qd[kThreads / 64][kQd][64];
+  int32_t qi[kThreads / 64][5][64];   // imin, jmin, nw, key, start
+};
+
 __global__ void __launch_bounds__(kThreads)
 rectify_claim_kernel(RectArgs a) {
   extern __shared__ __align__(16) unsigned char smem[];
-  int64_t* offs_s = reinterpret_cast<int64_t*>(smem);
+  ClaimLds& L = *reinterpret_cast<ClaimLds*>(smem);
+  int64_t* offs_s = reinterpret_cast<int64_t*>(smem + sizeof(ClaimLds));
   const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const bool lds_offs = a.ntiles <= kOffsLds;
   if (lds_offs)
     for (int64_t t = threadIdx.x; t <= a.ntiles; t += kThreads) offs_s[t] = a.chunk_offs[t];
   __syncthreads();
   const int64_t* offs = lds_offs ? offs_s : a.chunk_offs;
   const int64_t nchunks = offs[a.ntiles];
+  const double umin = -a.uv_delta, uvmax = 1.0 + 2 * a.uv_delta;
   for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
     int64_t lo = 0, hi = a.ntiles;   // last t with offs[t] <= c
     while (hi - lo > 1) {
@@ -363,59 +377,105 @@ rectify_claim_kernel(RectArgs a) {
       if (offs[m] <= c) lo = m; else hi = m;
     }
     const TileInfo ti = a.tiles[lo];
-    const int64_t nq_i = ti.swin - 1;
+    const int32_t nq_i = ti.swin - 1;
     const int64_t q = (c - offs[lo]) * kThreads + threadIdx.x;
-    const bool valid = ti.si0 >= 0 && nq_i > 0 && q < nq_i * (int64_t)(ti.shin - 1);
-    int64_t lj = 0, li = 0, qj = 0, qi = 0;
+    const bool valid = ti.si0 >= 0 && nq_i > 0 && q < (int64_t)nq_i * (int64_t)(ti.shin - 1);
+    int32_t lj = 0, li = 0, qj = 0, qi = 0;
     Quad Q{NAN, NAN, NAN, NAN, NAN, NAN, NAN, NAN};
     int64_t pi0 = 0, pj0 = 0, pi2 = 0, pj2 = 0;
     if (valid) {
-      lj = q / nq_i;
-      li = q - lj * nq_i;                     // quad within the tile window
+      lj = (int32_t)(q / nq_i);
+      li = (int32_t)(q - (int64_t)lj * nq_i);  // quad within the tile window
       qj = ti.sj0 + lj;
-      qi = ti.si0 + li;                       // global quad corner p0
-      const int64_t r0 = qj * a.sy, r1 = (qj + 1) * a.sy;
+      qi = ti.si0 + li;                        // global quad corner p0
+      const int64_t r0 = (int64_t)qj * a.sy, r1 = (int64_t)(qj + 1) * a.sy;
       Q.x0 = a.x[r0 + qi]; Q.y0 = a.y[r0 + qi];
       Q.x2 = a.x[r1 + qi]; Q.y2 = a.y[r1 + qi];
-      pi0 = pix_fast(Q.x0, ti.x_off, a.x_scale, a.inv_x, a.margin); pj0 = pix_fast(Q.y0, ti.y_off, a.y_scale, a.inv_y, a.margin);
-      pi2 = pix_fast(Q.x2, ti.x_off, a.x_scale, a.inv_x, a.margin); pj2 = pix_fast(Q.y2, ti.y_off, a.y_scale, a.inv_y, a.margin);
+      pi0 = pix_fast(Q.x0, ti.x_off, a.x_scale, a.inv_x, a.margin);
+      pj0 = pix_fast(Q.y0, ti.y_off, a.y_scale, a.inv_y, a.margin);
+      pi2 = pix_fast(Q.x2, ti.x_off, a.x_scale, a.inv_x, a.margin);
+      pj2 = pix_fast(Q.y2, ti.y_off, a.y_scale, a.inv_y, a.margin);
     }
     // right-hand corners from the next lane (all lanes take part in shuffles)
     Q.x1 = __shfl_down(Q.x0, 1, 64); Q.y1 = __shfl_down(Q.y0, 1, 64);
     Q.x3 = __shfl_down(Q.x2, 1, 64); Q.y3 = __shfl_down(Q.y2, 1, 64);
     int64_t pi1 = __shfl_down(pi0, 1, 64), pj1 = __shfl_down(pj0, 1, 64);
     int64_t pi3 = __shfl_down(pi2, 1, 64), pj3 = __shfl_down(pj2, 1, 64);
-    if (!valid) continue;
-    if (lane == 63 || li + 1 >= nq_i) {       // neighbour lane is not quad (lj, li+1)
-      const int64_t r0 = qj * a.sy, r1 = (qj + 1) * a.sy;
-      Q.x1 = a.x[r0 + qi + 1]; Q.y1 = a.y[r0 + qi + 1];
-      Q.x3 = a.x[r1 + qi + 1]; Q.y3 = a.y[r1 + qi + 1];
-      pi1 = pix_fast(Q.x1, ti.x_off, a.x_scale, a.inv_x, a.margin); pj1 = pix_fast(Q.y1, ti.y_off, a.y_scale, a.inv_y, a.margin);
-      pi3 = pix_fast(Q.x3, ti.x_off, a.x_scale, a.inv_x, a.margin); pj3 = pix_fast(Q.y3, ti.y_off, a.y_scale, a.inv_y, a.margin);
-    }
-    int64_t imin = min(min(pi0, pi1), min(pi2, pi3)), imax = max(max(pi0, pi1), max(pi2, pi3));
-    int64_t jmin = min(min(pj0, pj1), min(pj2, pj3)), jmax = max(max(pj0, pj1), max(pj2, pj3));
-    if (imax < 0 || jmax < 0 || imin >= ti.tw || jmin >= ti.th) continue;
-    imin = max(imin, (int64_t)0); jmin = max(jmin, (int64_t)0);
-    imax = min(imax, (int64_t)ti.tw - 1); jmax = min(jmax, (int64_t)ti.th - 1);
-    double det_a, det_b;
-    quad_dets(Q, det_a, det_b);
-    if (det_a == 0.0 && det_b == 0.0) continue;
-    const double ra = det_a != 0.0 ? 1.0 / det_a : 0.0, rb = det_b != 0.0 ? 1.0 / det_b : 0.0;
-    const double umin = -a.uv_delta, uvmax = 1.0 + 2 * a.uv_delta;
-    const uint32_t key = (uint32_t)(qj * a.w + qi);
-    for (int64_t dj = jmin; dj <= jmax; ++dj) {
-      const double dy = ti.y_off + ((double)dj + 0.5) * a.y_scale;
-      uint32_t* krow = a.keys + (int64_t)(ti.r0 + dj) * a.dst_w + ti.c0;
-      for (int64_t di = imin; di <= imax; ++di) {
-        if (PREREAD && krow[di] <= key) continue;  // already claimed by an earlier quad
-        const double dx = ti.x_off + ((double)di + 0.5) * a.x_scale;
-        const bool hit =
-            tri_hit_fast(dx, dy, Q.x0, Q.y0, Q.x2, Q.y2, Q.x1, Q.y1, det_a, ra, umin, uvmax, a.margin) ||
-            tri_hit_fast(dx, dy, Q.x3, Q.y3, Q.x1, Q.y1, Q.x2, Q.y2, det_b, rb, umin, uvmax, a.margin);
-        if (hit) atomicMin(&krow[di], key);
+    int32_t cnt = 0, imin32 = 0, jmin32 = 0, nw = 1;
+    double det_a = 0.0, det_b = 0.0;
+    if (valid) {
+      if (lane == 63 || li + 1 >= nq_i) {      // neighbour lane is not quad (lj, li+1)
+        const int64_t r0 = (int64_t)qj * a.sy, r1 = (int64_t)(qj + 1) * a.sy;
+        Q.x1 = a.x[r0 + qi + 1]; Q.y1 = a.y[r0 + qi + 1];
+        Q.x3 = a.x[r1 + qi + 1]; Q.y3 = a.y[r1 + qi + 1];
+        pi1 = pix_fast(Q.x1, ti.x_off, a.x_scale, a.inv_x, a.margin);
+        pj1 = pix_fast(Q.y1, ti.y_off, a.y_scale, a.inv_y, a.margin);
+        pi3 = pix_fast(Q.x3, ti.x_off, a.x_scale, a.inv_x, a.margin);
+        pj3 = pix_fast(Q.y3, ti.y_off, a.y_scale, a.inv_y, a.margin);
+      }
+      int64_t imin = min(min(pi0, pi1), min(pi2, pi3)), imax = max(max(pi0, pi1), max(pi2, pi3));
+      int64_t jmin = min(min(pj0, pj1), min(pj2, pj3)), jmax = max(max(pj0, pj1), max(pj2, pj3));
+      if (!(imax < 0 || jmax < 0 || imin >= ti.tw || jmin >= ti.th)) {
+        imin = max(imin, (int64_t)0); jmin = max(jmin, (int64_t)0);
+        imax = min(imax, (int64_t)ti.tw - 1); jmax = min(jmax, (int64_t)ti.th - 1);
+        quad_dets(Q, det_a, det_b);
+        if (!(det_a == 0.0 && det_b == 0.0)) {
+          imin32 = (int32_t)imin;
+          jmin32 = (int32_t)jmin;
+          nw = (int32_t)(imax - imin + 1);
+          cnt = nw * (int32_t)(jmax - jmin + 1);
+        }
       }
     }
+    // wave-exclusive prefix sum of the window sizes
+    int32_t incl = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int32_t v = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += v;
+    }
+    const int32_t total = __shfl(incl, 63, 64);
+    if (total == 0) continue;
+    double* qd = &L.qd[wv][0][0];
+    int32_t* qs = &L.qi[wv][0][0];
+    qd[0 * 64 + lane] = Q.x0; qd[1 * 64 + lane] = Q.y0;
+    qd[2 * 64 + lane] = Q.x1; qd[3 * 64 + lane] = Q.y1;
+    qd[4 * 64 + lane] = Q.x2; qd[5 * 64 + lane] = Q.y2;
+    qd[6 * 64 + lane] = Q.x3; qd[7 * 64 + lane] = Q.y3;
+    qd[8 * 64 + lane] = det_a; qd[9 * 64 + lane] = det_b;
+    qd[10 * 64 + lane] = det_a != 0.0 ? 1.0 / det_a : 0.0;
+    qd[11 * 64 + lane] = det_b != 0.0 ? 1.0 / det_b : 0.0;
+    qs[0 * 64 + lane] = imin32; qs[1 * 64 + lane] = jmin32; qs[2 * 64 + lane] = nw;
+    qs[3 * 64 + lane] = (int32_t)((int64_t)qj * a.w + qi);
+    qs[4 * 64 + lane] = incl - cnt;   // exclusive start
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int32_t k = lane; k < total; k += 64) {
+      int32_t o = 0;                   // owner: last lane with start <= k
+#pragma unroll
+      for (int step = 32; step > 0; step >>= 1)
+        if (qs[4 * 64 + o + step] <= k) o += step;
+      const int32_t local = k - qs[4 * 64 + o];
+      const int32_t w_ = qs[2 * 64 + o];
+      const int32_t dj_ = (int32_t)(((float)local + 0.5f) / (float)w_);
+      const int32_t di = qs[0 * 64 + o] + (local - dj_ * w_);
+      const int32_t dj = qs[1 * 64 + o] + dj_;
+      const double x0 = qd[0 * 64 + o], y0 = qd[1 * 64 + o], x1 = qd[2 * 64 + o],
+                   y1 = qd[3 * 64 + o], x2 = qd[4 * 64 + o], y2 = qd[5 * 64 + o],
+                   x3 = qd[6 * 64 + o], y3 = qd[7 * 64 + o];
+      const double dy = ti.y_off + ((double)dj + 0.5) * a.y_scale;
+      const double dx = ti.x_off + ((double)di + 0.5) * a.x_scale;
+      const bool hit =
+          tri_hit_fast(dx, dy, x0, y0, x2, y2, x1, y1, qd[8 * 64 + o], qd[10 * 64 + o], umin,
+                       uvmax, a.margin) ||
+          tri_hit_fast(dx, dy, x3, y3, x1, y1, x2, y2, qd[9 * 64 + o], qd[11 * 64 + o], umin,
+                       uvmax, a.margin);
+      if (hit)
+        atomicMin(a.keys + (int64_t)(ti.r0 + dj) * a.dst_w + ti.c0 + di,
+                  (uint32_t)qs[3 * 64 + o]);
+    }
+    __builtin_amdgcn_wave_barrier();   // the next chunk rewrites this wave's LDS slots
   }
 }
 
@@ -648,23 +708,15 @@ extern "C" int xrs_rectify_ij(const double* x, const double* y, int64_t h, int64
   hipStream_t st = static_cast<hipStream_t>(stream);
   XRS_HIP_CHECK(hipMemsetAsync(keys, 0xFF, (size_t)(dst_h * dst_w) * sizeof(uint32_t), st));
   {
-    // A/B knobs: XRS_RECTIFY_PREREAD (skip quads whose pixel is already
-    // claimed by a smaller key), XRS_RECTIFY_BLOCKS_PER_CU (0 = one chunk per
-    // block when the caller knows the chunk count, else 16 blocks per CU)
-    const char* pr = getenv("XRS_RECTIFY_PREREAD");
+    // A/B knob: XRS_RECTIFY_BLOCKS_PER_CU (0 = one chunk per block when the
+    // caller knows the chunk count, else 16 blocks per CU)
     const char* bpc = getenv("XRS_RECTIFY_BLOCKS_PER_CU");
-    // measured (config 4): no pre-read 2.04 ms vs 3.42 ms (the dependent read
-    // is latency on every tested pixel, the atomicMin is fire-and-forget);
-    // one chunk per block 1.98 vs 2.04 ms
-    const bool preread = pr ? atoi(pr) != 0 : false;
     const int cap = bpc && atoi(bpc) > 0 ? 256 * atoi(bpc) : (1 << 24);
     const int nb = max_chunks > 0 ? grid_blocks(max_chunks, 1, cap)
                                   : grid_blocks(256 * 16, 1, cap);
-    const size_t lds = ntiles <= kOffsLds ? (size_t)(ntiles + 1) * sizeof(int64_t) : 0;
-    if (preread)
-      hipLaunchKernelGGL(rectify_claim_kernel<true>, dim3(nb), dim3(kThreads), lds, st, a);
-    else
-      hipLaunchKernelGGL(rectify_claim_kernel<false>, dim3(nb), dim3(kThreads), lds, st, a);
+    const size_t lds = sizeof(ClaimLds) +
+                       (ntiles <= kOffsLds ? (size_t)(ntiles + 1) * sizeof(int64_t) : 0);
+    hipLaunchKernelGGL(rectify_claim_kernel, dim3(nb), dim3(kThreads), lds, st, a);
     XRS_HIP_CHECK(hipGetLastError());
   }
   const int nb2 = grid_blocks(dst_h * dst_w, kThreads, 256 * 8);
