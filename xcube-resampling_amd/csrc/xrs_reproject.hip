@@ -314,7 +314,8 @@ gather_separable_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t bands_
 // No carried rows: every target row loads its two source rows (the ceil/floor
 // overlap of neighbouring rows is served by L1/L2), but the loads of kRowsB
 // rows are independent and in flight together (memory-level parallelism).
-template <typename T, typename O, int INTERP, int kRowsB, bool NT = false, int PX = kPx>
+template <typename T, typename O, int INTERP, int kRowsB, bool NT = false, int PX = kPx,
+          int DBG = 0>
 __global__ void __launch_bounds__(kThreads)
 gather_separable_mlp_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t bands_per_tile,
                             int64_t segs_per_tile, int64_t nwork) {
@@ -376,7 +377,8 @@ gather_separable_mlp_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t ba
               const T v01 = (okf && xc) ? v[q][1][k] : fill;
               const T v10 = (okc && xf) ? v[q][2][k] : fill;
               const T v11 = (okc && xc) ? v[q][3][k] : fill;
-              out = Conv<O>::from_f64(interp4<T, INTERP>(v00, v01, v10, v11, dx[k], ye[q].d));
+              if (DBG == 1) out = (O)(v00 + v01 + v10 + v11);
+              else out = Conv<O>::from_f64(interp4<T, INTERP>(v00, v01, v10, v11, dx[k], ye[q].d));
             }
             if (lc < ncols) {
               if (NT) __builtin_nontemporal_store(out, &dst[(r + q) * a.dst_sy + lc]);
@@ -712,6 +714,224 @@ gather_staged_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t bands_per
   }
 }
 
+// ---- K1w: wave-staged separable gather -------------------------------------
+// bilinear from 4-byte gathers issues 4 vector-memory instructions per target
+// pixel and is bound by that issue rate (PMC: WAIT_INST dominates; nearest,
+// 1 tap, streams at 6.4 TB/s).  Here each wave owns 256 consecutive target
+// columns (4 per lane) of a band of rows.  The source rows the band needs are
+// staged ONCE per wave into a private LDS ring with aligned 16-byte loads —
+// one vector-memory instruction moves 256 source elements — in bursts of the
+// rows needed by G target rows (all loads of a burst in flight together);
+// the taps are then LDS reads and each lane writes its 4 pixels with one
+// vector store.  No block-level synchronisation: the ring is wave-private.
+// Falls back to 4-byte global taps (same arithmetic) for a burst whose rows
+// are not increasing or do not fit the ring, and for a wave whose column
+// span exceeds the stage width.
+constexpr int kWsW = 320;     // staged elements per source row and wave
+constexpr int kWsR = 8;       // ring rows per wave
+constexpr int kWsG = 4;       // target rows per staging burst
+
+template <typename T, typename O, int INTERP, bool VEC_ST>
+__global__ void __launch_bounds__(kThreads)
+gather_wave_staged_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t bands_per_tile,
+                          int64_t segs_per_tile, int64_t nwork) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  constexpr int E = 16 / (int)sizeof(T);       // elements per 16-byte load
+  constexpr int NV = kWsW / E;                 // 16-byte vectors per staged row
+  const Geometry& g = a.g;
+  const T fill = Conv<T>::from_f64(a.fill);
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  T* ring = reinterpret_cast<T*>(smem) + wv * (kWsR * kWsW);
+  const XcdSlice sl = xcd_slice(nwork);
+  for (int64_t w = sl.first; w < sl.end; w += sl.step) {
+    WorkItem it;
+    if (!work_item(g, w, ty0, nsegs, bands_per_tile, segs_per_tile, it)) continue;
+    const int64_t wc0 = it.c0 + 256 * wv;          // this wave's first target column
+    if (wc0 >= it.c1) continue;
+    const int ncols = (int)min((int64_t)256, it.c1 - wc0);
+    const AxisEntry* xt = a.xtab + it.t * g.tile_w + (wc0 - it.tx * g.tile_w);
+    int32_t cf[4], cc[4];
+    double dx[4];
+    int32_t lo = INT32_MAX, hi = -1;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int lc = 4 * lane + k;
+      AxisEntry e{-1, -1, 0.0};
+      if (lc < ncols) e = xt[lc];
+      cf[k] = e.f; cc[k] = e.c; dx[k] = e.d;
+      if (e.f >= 0) { lo = min(lo, e.f); hi = max(hi, e.f); }
+      if (INTERP != XRS_INTERP_NEAREST && e.c >= 0) { lo = min(lo, e.c); hi = max(hi, e.c); }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      lo = min(lo, __shfl_xor(lo, o, 64));
+      hi = max(hi, __shfl_xor(hi, o, 64));
+    }
+    lo = __builtin_amdgcn_readfirstlane(lo);
+    hi = __builtin_amdgcn_readfirstlane(hi);
+    const int32_t base = hi >= 0 ? lo - lo % E : 0;
+    const bool cols_fit = hi < 0 || hi - base < kWsW;
+    const int nvec = hi >= 0 ? (hi - base) / E + 1 : 0;
+    int32_t of[4], oc[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      of[k] = cf[k] >= 0 ? cf[k] - base : 0;
+      oc[k] = cc[k] >= 0 ? cc[k] - base : 0;
+    }
+    const AxisEntry* yt = a.ytab + it.t * g.tile_h - it.ty * g.tile_h;
+    for (int64_t sn = 0; sn < a.n; ++sn) {
+      const T* __restrict__ src = static_cast<const T*>(a.src) + sn * a.src_sn;
+      O* __restrict__ dst = static_cast<O*>(a.dst) + sn * a.dst_sn - g.row_begin * a.dst_sy + wc0;
+      // ring contents: every source row in [ring_lo, staged_hi] (at most the
+      // last kWsR of them) is staged; rows are only ever appended upwards.
+      // Software pipeline: the loads of burst b+1's new rows are issued before
+      // burst b is computed and land in LDS after it.
+      typedef unsigned int V __attribute__((ext_vector_type(4)));   // SROA-friendly
+      constexpr int NJ = (NV + 63) / 64;
+      int32_t staged_hi = INT32_MIN, ring_lo = 0;
+      AxisEntry ye[kWsG];
+      int nr = 0;
+      int32_t rlo = INT32_MAX, rhi = -1;
+      auto burst = [&](int64_t rb, AxisEntry (&e)[kWsG], int& n, int32_t& l, int32_t& h) {
+        n = (int)min((int64_t)kWsG, it.r1 - rb);
+        l = INT32_MAX; h = -1;
+#pragma unroll
+        for (int q = 0; q < kWsG; ++q) {
+          e[q] = q < n ? yt[rb + q] : AxisEntry{-1, -1, 0.0};
+          const int32_t f = e[q].f, c = INTERP != XRS_INTERP_NEAREST ? e[q].c : e[q].f;
+          if (f >= 0) { l = min(l, f); h = max(h, f); }
+          if (c >= 0) { l = min(l, c); h = max(h, c); }
+        }
+      };
+      // can rows [l, h] be served by the ring after appending (staged_hi, h]?
+      auto plan = [&](int32_t l, int32_t h, bool& cont) -> bool {
+        cont = staged_hi != INT32_MIN && l <= staged_hi + 1 &&
+               l >= max(ring_lo, staged_hi - (kWsR - 1));
+        return cols_fit && h >= 0 && h - l < kWsR && (cont || staged_hi == INT32_MIN || l > staged_hi);
+      };
+      auto load_rows = [&](int32_t s0, int nnew, V (&buf)[kWsR][NJ]) {
+#pragma unroll
+        for (int i = 0; i < kWsR; ++i) {
+          if (i < nnew) {
+            const T* row = src + (int64_t)(s0 + i) * a.src_sy + base;
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+              const int v = lane + 64 * j;
+              if (v < nvec) buf[i][j] = *reinterpret_cast<const V*>(row + v * E);
+            }
+          }
+        }
+      };
+      auto store_rows = [&](int32_t s0, int nnew, const V (&buf)[kWsR][NJ]) {
+#pragma unroll
+        for (int i = 0; i < kWsR; ++i) {
+          if (i < nnew) {
+            T* lrow = ring + ((s0 + i) % kWsR) * kWsW;
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+              const int v = lane + 64 * j;
+              if (v < nvec) *reinterpret_cast<V*>(lrow + v * E) = buf[i][j];
+            }
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      };
+      V buf[kWsR][NJ];
+      burst(it.r0, ye, nr, rlo, rhi);
+      bool use_ring;
+      {
+        bool cont;
+        use_ring = plan(rlo, rhi, cont);
+        if (use_ring) {
+          const int32_t s0 = cont ? staged_hi + 1 : rlo;
+          load_rows(s0, rhi - s0 + 1, buf);
+          store_rows(s0, rhi - s0 + 1, buf);
+          ring_lo = rlo; staged_hi = rhi;
+        }
+      }
+      for (int64_t r = it.r0; r < it.r1; r += kWsG) {
+        // next burst: entries, plan, loads in flight
+        AxisEntry yn[kWsG];
+        int nrn = 0;
+        int32_t rlon = INT32_MAX, rhin = -1;
+        const bool has_next = r + kWsG < it.r1;
+        bool next_ring = false, next_cont = false;
+        int32_t ns0 = 0;
+        int nnew = 0;
+        if (has_next) {
+          burst(r + kWsG, yn, nrn, rlon, rhin);
+          next_ring = plan(rlon, rhin, next_cont);
+          if (next_ring) {
+            ns0 = next_cont ? staged_hi + 1 : rlon;
+            nnew = rhin - ns0 + 1;
+            load_rows(ns0, nnew, buf);
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < kWsG; ++q) {
+          if (q >= nr) break;
+          const bool okf = ye[q].f >= 0, okc = ye[q].c >= 0;
+          T v[4][4];
+          if (use_ring) {
+            const T* lf = ring + ((okf ? ye[q].f : 0) % kWsR) * kWsW;
+            const T* lc = ring + ((okc ? ye[q].c : 0) % kWsR) * kWsW;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              v[0][k] = lf[of[k]];
+              if (INTERP != XRS_INTERP_NEAREST) { v[1][k] = lf[oc[k]]; v[2][k] = lc[of[k]]; v[3][k] = lc[oc[k]]; }
+            }
+          } else {
+            const T* rf = src + (int64_t)max(ye[q].f, 0) * a.src_sy;
+            const T* rc = src + (int64_t)max(ye[q].c, 0) * a.src_sy;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              const int32_t f = max(cf[k], 0), c = max(cc[k], 0);
+              v[0][k] = rf[f];
+              if (INTERP != XRS_INTERP_NEAREST) { v[1][k] = rf[c]; v[2][k] = rc[f]; v[3][k] = rc[c]; }
+            }
+          }
+          O out[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const bool xf = cf[k] >= 0, xc = cc[k] >= 0;
+            const T v00 = (okf && xf) ? v[0][k] : fill;
+            if (INTERP == XRS_INTERP_NEAREST) {
+              out[k] = (O)v00;
+            } else {
+              const T v01 = (okf && xc) ? v[1][k] : fill;
+              const T v10 = (okc && xf) ? v[2][k] : fill;
+              const T v11 = (okc && xc) ? v[3][k] : fill;
+              out[k] = Conv<O>::from_f64(interp4<T, INTERP>(v00, v01, v10, v11, dx[k], ye[q].d));
+            }
+          }
+          O* drow = dst + (r + q) * a.dst_sy + 4 * lane;
+          if (VEC_ST && 4 * lane + 3 < ncols) {
+            typedef O O4 __attribute__((ext_vector_type(4)));
+            O4 o4 = {out[0], out[1], out[2], out[3]};
+            __builtin_nontemporal_store(o4, reinterpret_cast<O4*>(drow));
+          } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+              if (4 * lane + k < ncols) __builtin_nontemporal_store(out[k], drow + k);
+          }
+        }
+        if (has_next) {
+          if (next_ring) {
+            store_rows(ns0, nnew, buf);
+            if (!next_cont) ring_lo = rlon;
+            if (nnew > 0) staged_hi = rhin;
+          }
+#pragma unroll
+          for (int q = 0; q < kWsG; ++q) ye[q] = yn[q];
+          nr = nrn;
+          use_ring = next_ring;
+        }
+      }
+    }
+  }
+}
+
 // Separable gather variant (XRS_REPROJECT_VARIANT, for A/B measurements; all
 // variants are bit-identical, only the load schedule differs):
 //   0      rows carried in registers (fewest loads, one source row in flight)
@@ -731,7 +951,14 @@ gather_staged_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t bands_per
 // Also measured and dropped: the two horizontal taps as one dword-aligned
 // 8-byte load (global_load_dwordx2 at odd addresses): 4.08 ms vs 2.69 ms.
 // Reference point on the same box: nearest (1 tap) 2.08 ms = 6.4 TB/s, a
-// torch copy_ of the raster 2.8 ms — bilinear is tap-issue bound, not HBM.
+// torch copy_ of the raster 2.8 ms — bilinear is tap-issue bound, not HBM
+// (PMC: SQ_WAIT_INST_ANY > SQ_WAIT_ANY; dropping the f64 lerps, keeping the 4
+// taps, changes nothing: 2.63 vs 2.68 ms).
+//   20     wave-staged: 256 columns per wave, source rows staged once into a
+//          wave-private LDS ring by 16-byte loads, software-pipelined bursts
+//          of 4 target rows, one 16-byte store per lane and row: 3.48 ms
+//          (12: 2.56 ms) — the LDS round trip and 168 VGPRs cost more than the
+//          saved gathers; lane-strided pixels with dword stores: 3.85 ms.
 inline int variant() {
   const char* v = getenv("XRS_REPROJECT_VARIANT");
   return v ? atoi(v) : 12;
@@ -748,7 +975,7 @@ int launch(const GatherArgs& a, int coord_mode, AxisEntry* xtab, AxisEntry* ytab
   if (variant() == 14 && args.g.band > 64) args.g.band = 64;   // rows_s capacity
   const int64_t bands_per_tile = (g.tile_h + args.g.band - 1) / args.g.band;
   const int v = variant();
-  args.g.segw = kThreads * (v == 9 || v == 12 || v == 13 || v == 14 ? 2 : v == 10 ? 8 : v == 11 ? 1 : kPx);
+  args.g.segw = kThreads * (v == 9 || v == 12 || v == 13 || v == 14 || v == 90 ? 2 : v == 10 ? 8 : v == 20 ? 4 : v == 11 ? 1 : kPx);
   const int64_t segs_per_tile = (g.tile_w + args.g.segw - 1) / args.g.segw;
   const int64_t nsegs = g.ntiles_x * segs_per_tile;
   const int64_t nwork = (ty1 - ty0) * bands_per_tile * nsegs;
@@ -805,6 +1032,30 @@ int launch(const GatherArgs& a, int coord_mode, AxisEntry* xtab, AxisEntry* ytab
                          segs_per_tile, nwork);
     else if (v == 13)
       hipLaunchKernelGGL((gather_separable_mlp_kernel<T, O, INTERP, 16, true, 2>), dim3(nb),
+                         dim3(kThreads), 0, stream, args, ty0, nsegs, bands_per_tile,
+                         segs_per_tile, nwork);
+    else if (v == 20) {
+      // wave-staged: 16-byte staging loads need 16-byte aligned source rows
+      const int esz = (int)sizeof(T);
+      const bool aligned = (16 % esz == 0) && ((uintptr_t)a.src % 16 == 0) &&
+                           ((a.src_sy * esz) % 16 == 0) && ((a.src_sn * esz) % 16 == 0);
+      const bool vst = ((uintptr_t)a.dst % (4 * sizeof(O)) == 0) && (a.dst_sy % 4 == 0) &&
+                       (a.dst_sn % 4 == 0) && (g.tile_w % 4 == 0);
+      const size_t lds = (size_t)4 * kWsR * kWsW * sizeof(T);
+      if (!aligned)
+        hipLaunchKernelGGL((gather_separable_mlp_kernel<T, O, INTERP, 8, true, 2>), dim3(nb),
+                           dim3(kThreads), 0, stream, args, ty0, nsegs, bands_per_tile,
+                           segs_per_tile, nwork);
+      else if (vst)
+        hipLaunchKernelGGL((gather_wave_staged_kernel<T, O, INTERP, true>), dim3(nb),
+                           dim3(kThreads), lds, stream, args, ty0, nsegs, bands_per_tile,
+                           segs_per_tile, nwork);
+      else
+        hipLaunchKernelGGL((gather_wave_staged_kernel<T, O, INTERP, false>), dim3(nb),
+                           dim3(kThreads), lds, stream, args, ty0, nsegs, bands_per_tile,
+                           segs_per_tile, nwork);
+    } else if (v == 90)   // timing probe only: bilinear loads, f32 sum instead of the f64 lerps
+      hipLaunchKernelGGL((gather_separable_mlp_kernel<T, O, INTERP, 8, true, 2, 1>), dim3(nb),
                          dim3(kThreads), 0, stream, args, ty0, nsegs, bands_per_tile,
                          segs_per_tile, nwork);
     else if (v == 14) {
