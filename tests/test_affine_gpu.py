@@ -204,3 +204,48 @@ def test_reduce_lds_stage_knob_bit_identical(stage, monkeypatch):
         got = A._resample_array(a, None, None, m, oshape, ochunks, 1, agg, recover, fill)
         got = got if isinstance(got, np.ndarray) else got.cpu().numpy()
         assert_bitwise_equal(got, np.asarray(ref), f"stage={stage} seed {seed} {agg}")
+
+
+@pytest.mark.parametrize("k3i", ["1", "0"])
+@pytest.mark.parametrize("dtype,nd", [(np.float32, 2), (np.float64, 2), (np.float32, 3),
+                                      (np.float64, 3)])
+def test_integral_coarsen_k3i_matches_oracle(k3i, dtype, nd, monkeypatch):
+    """K3i (the integral-grid coarsen kernel: square factors 2/4/8 whose div-x
+    grid sits on source pixels) and the generic K3 (XRS_AFFINE_INTEGRAL=0) are
+    both bit-exact with the oracle: order 0 and 1, integral offsets incl.
+    misaligned vector starts and targets reaching past the source (cval /
+    exact path at the edges), NaN / +-inf / -0.0 in the taps, the zero-weight
+    time neighbour of 3-D inputs, chunk edges (mirrored taps), widths that
+    are not a multiple of the 256-column block; a fractional offset (tables
+    not integral) routes to the generic K3."""
+    import xcube_resampling_amd.affine as A
+    from oracle import affine_ref
+
+    monkeypatch.setenv("XRS_AFFINE_INTEGRAL", k3i)
+    rng = np.random.default_rng(4242)
+    lead = (3,) if nd == 3 else ()
+    cases = [(4, (0.0, 0.0), (70, 300), (32, 128), 1, "mean"),
+             (4, (1.0, 3.0), (64, 270), (17, 270), 1, "mean"),
+             (2, (-2.0, 5.0), (90, 140), (30, 64), 1, "sum"),
+             (8, (8.0, -1.0), (20, 40), (8, 40), 1, "max"),
+             (4, (0.0, 2.0), (50, 66), (25, 33), 0, "mean"),
+             (2, (3.0, 0.0), (33, 515), (33, 515), 0, "min"),
+             (4, (0.5, 0.0), (40, 60), (20, 60), 1, "mean")]
+    for d, (ox, oy), oshape, tile, order, agg in cases:
+        shp = lead + (oshape[0] * d + 6, oshape[1] * d + 3)
+        a = (rng.random(shp) * 4 - 2).astype(dtype)
+        flat = a.reshape(-1)
+        idx = rng.choice(flat.size, max(4, flat.size // 400), replace=False)
+        q = idx.size // 4
+        flat[idx[:q]] = np.nan
+        flat[idx[q:2 * q]] = np.inf
+        flat[idx[2 * q:3 * q]] = -np.inf
+        flat[idx[3 * q:]] = -0.0
+        m = ((float(d), 0.0, ox), (0.0, float(d), oy))
+        ochunks = tuple(1 for _ in lead) + tile
+        ref = affine_ref.resample_array(a, m, lead + oshape, ochunks, order, agg, False, np.nan)
+        got = A._resample_array(a, None, None, m, lead + oshape, ochunks, order, agg, False,
+                                np.nan)
+        got = got if isinstance(got, np.ndarray) else got.cpu().numpy()
+        assert_bitwise_equal(got, np.asarray(ref), f"k3i={k3i} {dtype} d={d} off={ox},{oy} "
+                                                   f"order={order} {agg}")

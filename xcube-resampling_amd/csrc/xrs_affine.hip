@@ -95,15 +95,35 @@ __device__ inline AxisTab axis_entry(const AxisChunks& a, int64_t o) {
 }
 
 template <int ORDER>
+__device__ inline bool integral_entry(const AxisTab& e, int32_t g_first, int k) {
+  return e.g0 >= 0 && e.g0 == g_first + k &&
+         (ORDER == 0 || (e.w1 == 0.0 && e.g1 == e.g0 + 1));
+}
+
+// With `nonint` (K3i candidates, div dy x dx): also flag whether any in-bounds
+// entry breaks the integral-contiguous layout K3i's fast path needs (entry k of
+// a pixel's run = first entry + k, order 1: weight 0 and the next tap at +1).
+template <int ORDER>
 __global__ void __launch_bounds__(kThreads)
 affine_tables_kernel(AxisChunks ay, AxisChunks ax, AxisTab* __restrict__ ytab,
-                     AxisTab* __restrict__ xtab) {
+                     AxisTab* __restrict__ xtab, int64_t dy, int64_t dx,
+                     int32_t* __restrict__ nonint) {
   const int64_t total = ay.n + ax.n;
+  bool broken = false;
   for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * kThreads) {
-    if (i < ay.n) ytab[i] = axis_entry<ORDER>(ay, i);
-    else xtab[i - ay.n] = axis_entry<ORDER>(ax, i - ay.n);
+    const bool is_y = i < ay.n;
+    const int64_t o = is_y ? i : i - ay.n;
+    const AxisChunks& ac = is_y ? ay : ax;
+    const AxisTab e = axis_entry<ORDER>(ac, o);
+    (is_y ? ytab : xtab)[o] = e;
+    if (nonint && e.g0 >= 0) {
+      const int64_t d = is_y ? dy : dx, k = o % d;
+      const AxisTab f = k ? axis_entry<ORDER>(ac, o - k) : e;
+      broken = broken || f.g0 < 0 || !integral_entry<ORDER>(e, f.g0, (int)k);
+    }
   }
+  if (nonint && __any(broken) && (threadIdx.x & 63) == 0) atomicOr(nonint, 1);
 }
 
 // ---- scipy output casts ----------------------------------------------------
@@ -391,12 +411,87 @@ __device__ inline void fill_band(const AffineArgs& a, const R& p,
   }
 }
 
+// numpy's nan-reducers over one output pixel's dy x dx sub-samples in dask
+// chunk.coarsen order (coarsen.py:72-111): each sub-sample row is one pairwise
+// add.reduce, rows accumulated sequentially; integers accumulate in int64 /
+// float64 and the mean is rint-ed back (coarsen.py:104-110).
+template <typename I, bool FLOAT = std::is_floating_point<I>::value>
+struct Fold {
+  I total = (I)0.0, prod = (I)1.0, mx = (I)0.0;
+  int64_t cnt = 0, nonzero = 0;
+  bool have = false;
+  template <typename F>
+  __device__ inline void add_row(int agg, int nx, F&& get) {
+    auto val = [&](int si) -> I {
+      const I v = get(si);
+      const bool nan = v != v;
+      cnt += nan ? 0 : 1;
+      nonzero += (v != (I)0.0) ? 1 : 0;
+      prod = prod * (nan ? (I)1.0 : v);
+      if (agg == AGG_MAX) {  // np.fmax.reduce
+        if (!have) { mx = v; have = true; }
+        else mx = (mx >= v || nan) ? mx : v;
+      } else if (agg == AGG_MIN) {
+        if (!have) { mx = v; have = true; }
+        else mx = (mx <= v || nan) ? mx : v;
+      }
+      return nan ? (I)0.0 : v;
+    };
+    total = total + pairwise_row<I>(nx, val);
+  }
+  __device__ inline void store(const AffineArgs& a, int64_t didx) const {
+    double res;
+    if (a.agg == AGG_MEAN) res = (double)(I)((double)total / (double)cnt);
+    else if (a.agg == AGG_SUM) res = (double)total;
+    else if (a.agg == AGG_PROD) res = (double)prod;
+    else res = (double)mx;
+    if (a.agg == AGG_COUNT) store_any(a.dst, didx, a.dst_dtype, 0.0, nonzero, true);
+    else store_any(a.dst, didx, a.dst_dtype, res, 0, false);
+  }
+};
+template <typename I>
+struct Fold<I, false> {
+  double dtotal = 0.0;
+  int64_t nonzero = 0, isum = 0, iprod = 1, imx = 0, n = 0;
+  bool have = false;
+  template <typename F>
+  __device__ inline void add_row(int agg, int nx, F&& get) {
+    auto val = [&](int si) -> double {
+      const I v = get(si);
+      isum += (int64_t)v;
+      iprod *= (int64_t)v;
+      nonzero += v != 0 ? 1 : 0;
+      if (!have) { imx = (int64_t)v; have = true; }
+      else if (agg == AGG_MAX) imx = max(imx, (int64_t)v);
+      else if (agg == AGG_MIN) imx = min(imx, (int64_t)v);
+      return (double)v;
+    };
+    dtotal = dtotal + pairwise_row<double>(nx, val);
+    n += nx;
+  }
+  __device__ inline void store(const AffineArgs& a, int64_t didx) const {
+    if (a.agg == AGG_MEAN) {
+      const double m = rint(dtotal / (double)n);
+      store_any(a.dst, didx, a.dst_dtype, 0.0, (int64_t)Conv<I>::from_f64(m), true);
+    } else if (a.agg == AGG_SUM) {
+      store_any(a.dst, didx, a.dst_dtype, 0.0, isum, true);
+    } else if (a.agg == AGG_PROD) {
+      store_any(a.dst, didx, a.dst_dtype, 0.0, iprod, true);
+    } else if (a.agg == AGG_COUNT) {
+      store_any(a.dst, didx, a.dst_dtype, 0.0, nonzero, true);
+    } else {
+      store_any(a.dst, didx, a.dst_dtype, 0.0, imx, true);
+    }
+  }
+};
+
 template <typename T, typename I, int ORDER, bool RECOVER, int KB>
 __global__ void __launch_bounds__(kThreads)
 affine_reduce_kernel(AffineArgs a, const AxisTab* __restrict__ ytab,
                      const AxisTab* __restrict__ xtab, int group,
                      const int32_t* __restrict__ yb, const int32_t* __restrict__ xb,
-                     int stage_cap, int stage_bytes) {
+                     int stage_cap, int stage_bytes, const int32_t* __restrict__ nonint) {
+  if (nonint && !*nonint) return;   // K3i (launched before this one) did the work
   extern __shared__ __align__(16) unsigned char smem[];
   T* stage0 = reinterpret_cast<T*>(smem);
   T* stage1 = stage0 + stage_cap;
@@ -470,12 +565,7 @@ affine_reduce_kernel(AffineArgs a, const AxisTab* __restrict__ ytab,
       __syncthreads();
     }
 
-    // per-thread reducer state
-    I total = (I)0.0, prod = (I)1.0, mx = (I)0.0;
-    double dtotal = 0.0;
-    int64_t cnt = 0, nonzero = 0, isum = 0, iprod = 1, imx = 0;
-    bool have = false;
-
+    Fold<I> fold;
     for (int s0 = 0; s0 < ny; s0 += group) {
       const int g_n = min(group, ny - s0);
       // (A) sub-samples of rows s0 .. s0+g_n-1 into the band
@@ -500,66 +590,176 @@ affine_reduce_kernel(AffineArgs a, const AxisTab* __restrict__ ytab,
         for (int g = 0; g < g_n; ++g) {
           const I* brow = buf + (ty * g_n + g) * row_stride;
           const int kb = tx * nx;
-          if (std::is_floating_point<I>::value) {
-            auto val = [&](int si) -> I {
-              const I v = brow[lds_pos(kb + si)];
-              const bool nan = v != v;
-              cnt += nan ? 0 : 1;
-              nonzero += (v != (I)0.0) ? 1 : 0;
-              prod = prod * (nan ? (I)1.0 : v);
-              if (a.agg == AGG_MAX) {  // np.fmax.reduce
-                if (!have) { mx = v; have = true; }
-                else mx = (mx >= v || nan) ? mx : v;
-              } else if (a.agg == AGG_MIN) {
-                if (!have) { mx = v; have = true; }
-                else mx = (mx <= v || nan) ? mx : v;
-              }
-              return nan ? (I)0.0 : v;
-            };
-            total = total + pairwise_row<I>(nx, val);
-          } else {
-            auto val = [&](int si) -> double {
-              const I v = brow[lds_pos(kb + si)];
-              isum += (int64_t)v;
-              iprod *= (int64_t)v;
-              nonzero += v != 0 ? 1 : 0;
-              if (!have) { imx = (int64_t)v; have = true; }
-              else if (a.agg == AGG_MAX) imx = max(imx, (int64_t)v);
-              else if (a.agg == AGG_MIN) imx = min(imx, (int64_t)v);
-              return (double)v;
-            };
-            dtotal = dtotal + pairwise_row<double>(nx, val);
-          }
+          fold.add_row(a.agg, nx, [&](int si) { return brow[lds_pos(kb + si)]; });
         }
       }
       __syncthreads();  // the next group overwrites the band
     }
 
     const int64_t oj = oj0 + ty, oi = oi0 + tx;
-    if (ty < rows && oi < a.out_w) {
-      const int64_t didx = t * a.dst_st + oj * a.dst_sy + oi;
-      if (std::is_floating_point<I>::value) {
-        double res;
-        if (a.agg == AGG_MEAN) res = (double)(I)((double)total / (double)cnt);
-        else if (a.agg == AGG_SUM) res = (double)total;
-        else if (a.agg == AGG_PROD) res = (double)prod;
-        else res = (double)mx;
-        if (a.agg == AGG_COUNT) store_any(a.dst, didx, a.dst_dtype, 0.0, nonzero, true);
-        else store_any(a.dst, didx, a.dst_dtype, res, 0, false);
+    if (ty < rows && oi < a.out_w) fold.store(a, t * a.dst_st + oj * a.dst_sy + oi);
+  }
+}
+
+// K3i: coarsen reducers when every sub-sample of a pixel sits on a source
+// pixel (scale 1 at the div-x grid with integral offsets — every aligned
+// integer-factor coarsen, config 3 — or any order-0 grid at scale 1).  A
+// sub-sample is then the source value itself (order 1: -0 -> +0, or NaN when
+// one of scipy's zero-weight taps is non-finite, see Taps::eval).  One thread
+// per output pixel, lanes on consecutive output columns: a sub-sample row is
+// one DX-wide vector load per lane (a wave reads 64*DX contiguous elements),
+// the (DY+1) x (DX+1) source rect holding every tap of the pixel is loaded
+// once (the tap column right of the run comes from the next lane, the tap row
+// below is carried to the next output row).  Pixels whose table entries are
+// not integral-contiguous, or whose rect holds a non-finite value, take the
+// exact per-sub-sample path (Taps) — same result, slower.
+constexpr int kIntRows = 4;   // output rows per work item
+
+template <typename T, int DX>
+__device__ inline void load_run(const T* p, bool vec, T (&v)[DX]) {
+  constexpr int B = DX * (int)sizeof(T) >= 16 ? 16 : DX * (int)sizeof(T);
+  constexpr int PER = B / (int)sizeof(T);
+  typedef T V __attribute__((ext_vector_type(PER)));
+  if (vec) {
+#pragma unroll
+    for (int c = 0; c < DX / PER; ++c) {
+      const V x = *reinterpret_cast<const V*>(p + c * PER);
+#pragma unroll
+      for (int e = 0; e < PER; ++e) v[c * PER + e] = x[e];
+    }
+  } else {
+#pragma unroll
+    for (int c = 0; c < DX; ++c) v[c] = p[c];
+  }
+}
+
+template <typename T, int ORDER, int DY, int DX>
+__global__ void __launch_bounds__(kThreads)
+affine_reduce_integral_kernel(AffineArgs a, const AxisTab* __restrict__ ytab,
+                              const AxisTab* __restrict__ xtab, int vec_rows,
+                              const int32_t* __restrict__ nonint) {
+  if (*nonint) return;   // the generic K3 launched beside this one does the work
+  constexpr int NR = ORDER == 1 ? DY + 1 : DY;   // source rows of a pixel's rect
+  constexpr int B = DX * (int)sizeof(T) >= 16 ? 16 : DX * (int)sizeof(T);
+  const int lane = threadIdx.x & 63;
+  const int64_t ntx = (a.out_w + kThreads - 1) / kThreads;
+  const int64_t nty = (a.out_h + kIntRows - 1) / kIntRows;
+  const int64_t nwork = ntx * nty * a.nt;
+  const XcdSlice sl = xcd_slice(nwork);
+  for (int64_t w = sl.first; w < sl.end; w += sl.step) {
+    const int64_t t = w / (ntx * nty);
+    const int64_t rem = w - t * ntx * nty;
+    const int64_t tj = rem / ntx, ti = rem - tj * ntx;
+    const int64_t oi = ti * kThreads + threadIdx.x;
+    const bool active = oi < a.out_w;
+    const int64_t t1 = a.t_next ? a.t_next[t] : -1;
+    const bool two = ORDER == 1 && t1 >= 0;
+    Src<T> p;
+    p.g0 = static_cast<const T*>(a.src) + t * a.src_st;
+    p.g1 = two ? static_cast<const T*>(a.src) + t1 * a.src_st : p.g0;
+    p.sy = a.src_sy;
+
+    // columns (row-invariant): the pixel's DX sub-sample columns must be one
+    // contiguous run of source columns c0 .. c0+DX-1
+    bool col_fast = active;
+    int32_t c0 = 0;
+    if (active) {
+      const AxisTab e0 = xtab[oi * DX];
+      c0 = e0.g0;
+#pragma unroll
+      for (int si = 0; si < DX; ++si)
+        col_fast = col_fast && integral_entry<ORDER>(si ? xtab[oi * DX + si] : e0, c0, si);
+    }
+    const bool vec = vec_rows && ((int64_t)c0 * (int64_t)sizeof(T)) % B == 0;
+    // the tap column right of the run (order 1) from the next lane when that
+    // lane's run starts there
+    const int32_t c0n = __shfl_down(c0, 1);
+    const bool fast_n = __shfl_down((int)col_fast, 1) != 0;
+    const bool nb_lane = lane < 63 && fast_n && c0n == c0 + DX;
+
+    int32_t carry = -1;   // source row carried from the previous output row
+    T cv[DX], cv1[DX], cnb = (T)0, cnb1 = (T)0;
+    const int64_t oj_end = min(a.out_h, (tj + 1) * kIntRows);
+    for (int64_t oj = tj * kIntRows; oj < oj_end; ++oj) {
+      const AxisTab* yrow = ytab + oj * DY;
+      const AxisTab ey0 = yrow[0];
+      bool row_fast = true;
+#pragma unroll
+      for (int sj = 0; sj < DY; ++sj)
+        row_fast = row_fast && integral_entry<ORDER>(sj ? yrow[sj] : ey0, ey0.g0, sj);
+      Fold<T> fold;
+      bool slow = !col_fast || !row_fast;
+      if (row_fast) {   // block-uniform
+        const int32_t r0 = ey0.g0;
+        T v[NR][DX], v1[NR][DX], nb[NR], nb1[NR];
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+          if (ORDER == 1 && r == 0 && carry == r0) {
+#pragma unroll
+            for (int c = 0; c < DX; ++c) { v[0][c] = cv[c]; v1[0][c] = cv1[c]; }
+            nb[0] = cnb;
+            nb1[0] = cnb1;
+            continue;
+          }
+          if (col_fast) {   // other lanes take the exact path below
+            load_run<T, DX>(p.row0(r0 + r) + c0, vec, v[r]);
+            if (two) load_run<T, DX>(p.row1(r0 + r) + c0, vec, v1[r]);
+          }
+        }
+        if (ORDER == 1) {
+          bool bad = false;
+#pragma unroll
+          for (int r = 0; r < NR; ++r) {
+            if (!(ORDER == 1 && r == 0 && carry == r0)) {
+              const T sh = __shfl_down(v[r][0], 1);
+              nb[r] = nb_lane ? sh : (col_fast ? p.row0(r0 + r)[c0 + DX] : (T)0);
+              if (two) {
+                const T sh1 = __shfl_down(v1[r][0], 1);
+                nb1[r] = nb_lane ? sh1 : (col_fast ? p.row1(r0 + r)[c0 + DX] : (T)0);
+              }
+            }
+            bad = bad || !is_finite(nb[r]);
+            if (two) bad = bad || !is_finite(nb1[r]);
+#pragma unroll
+            for (int c = 0; c < DX; ++c) {
+              bad = bad || !is_finite(v[r][c]);
+              if (two) bad = bad || !is_finite(v1[r][c]);
+            }
+          }
+          slow = slow || bad;
+          carry = r0 + DY;
+#pragma unroll
+          for (int c = 0; c < DX; ++c) { cv[c] = v[DY][c]; cv1[c] = v1[DY][c]; }
+          cnb = nb[DY];
+          cnb1 = nb1[DY];
+        }
+        if (!slow) {
+#pragma unroll
+          for (int sj = 0; sj < DY; ++sj)
+            fold.add_row(a.agg, DX, [&](int si) {
+              const T x = v[sj][si];
+              return ORDER == 0 ? x : (x == (T)0 ? (T)0 : x);
+            });
+        }
       } else {
-        if (a.agg == AGG_MEAN) {
-          const double m = rint(dtotal / (double)(ny * nx));
-          store_any(a.dst, didx, a.dst_dtype, 0.0, (int64_t)Conv<T>::from_f64(m), true);
-        } else if (a.agg == AGG_SUM) {
-          store_any(a.dst, didx, a.dst_dtype, 0.0, isum, true);
-        } else if (a.agg == AGG_PROD) {
-          store_any(a.dst, didx, a.dst_dtype, 0.0, iprod, true);
-        } else if (a.agg == AGG_COUNT) {
-          store_any(a.dst, didx, a.dst_dtype, 0.0, nonzero, true);
-        } else {
-          store_any(a.dst, didx, a.dst_dtype, 0.0, imx, true);
+        carry = -1;
+      }
+      if (slow && active) {   // exact per-sub-sample evaluation (scipy's sum)
+        for (int sj = 0; sj < DY; ++sj) {
+          const AxisTab ey = yrow[sj];
+          fold.add_row(a.agg, DX, [&](int si) -> T {
+            const AxisTab ex = xtab[oi * DX + si];
+            Taps<T> tp;
+            if (two) {
+              tp.template load<ORDER, true>(p, ey, ex);
+              return tp.template eval<T, ORDER, false, true>(ey, ex, a.cval);
+            }
+            tp.template load<ORDER, false>(p, ey, ex);
+            return tp.template eval<T, ORDER, false, false>(ey, ex, a.cval);
+          });
         }
       }
+      if (active) fold.store(a, t * a.dst_st + oj * a.dst_sy + oi);
     }
   }
 }
@@ -572,74 +772,110 @@ inline int64_t reduce_row_bytes(int64_t dx, int64_t isize) {
   return (band_w + (band_w - 1) / 32) * isize;
 }
 
+// K3i candidates: square 2/4/8 coarsen factors of float rasters.  Whether the
+// tables really are integral is known on the device only (affine_tables_kernel
+// sets `nonint`), so K3i and the generic K3 are both launched and exactly one
+// of them works (the other returns at its first instruction).
+// A/B knob: XRS_AFFINE_INTEGRAL=0 forces the generic K3.
+template <typename T, typename I, bool RECOVER>
+inline bool integral_candidate(const AffineArgs& a) {
+  if (!std::is_floating_point<T>::value || !std::is_same<T, I>::value || RECOVER) return false;
+  if (a.dx != a.dy || (a.dx != 2 && a.dx != 4 && a.dx != 8)) return false;
+  const char* knob = std::getenv("XRS_AFFINE_INTEGRAL");
+  return !(knob && std::atoi(knob) == 0);
+}
+
 template <typename T, typename I, int ORDER, bool RECOVER>
 int launch(const AffineArgs& a, const AxisChunks& ay, const AxisChunks& ax, AxisTab* ytab,
-           AxisTab* xtab, int32_t* yb, int32_t* xb, hipStream_t st) {
+           AxisTab* xtab, int32_t* yb, int32_t* xb, int32_t* nonint, hipStream_t st) {
+  const bool direct = a.agg == AGG_NONE || a.agg == AGG_FIRST || a.agg == AGG_LAST ||
+                      a.agg == AGG_CENTER;
+  const bool k3i = !direct && integral_candidate<T, I, RECOVER>(a);
+  if (k3i) XRS_HIP_CHECK(hipMemsetAsync(nonint, 0, sizeof(int32_t), st));
   const int nbt = grid_blocks(ay.n + ax.n, kThreads, 1024);
   hipLaunchKernelGGL((affine_tables_kernel<ORDER>), dim3(nbt), dim3(kThreads), 0, st, ay, ax,
-                     ytab, xtab);
+                     ytab, xtab, a.dy, a.dx, k3i ? nonint : nullptr);
   XRS_HIP_CHECK(hipGetLastError());
   AffineArgs args = a;
   args.ytab = ytab;
   args.xtab = xtab;
-  const bool direct = a.agg == AGG_NONE || a.agg == AGG_FIRST || a.agg == AGG_LAST ||
-                      a.agg == AGG_CENTER;
   if (direct) {
     const int64_t ntiles =
         ((a.out_w + kTileW - 1) / kTileW) * ((a.out_h + kTileH - 1) / kTileH) * a.nt;
     const int nb = grid_blocks(ntiles, 1, 256 * 64);
     hipLaunchKernelGGL((affine_direct_kernel<T, I, ORDER, RECOVER>), dim3(nb), dim3(kThreads), 0,
                        st, args, ytab, xtab);
-  } else {
-    const int64_t row_bytes = reduce_row_bytes(a.dx, sizeof(I));
-    int64_t group = kReduceLdsBudget / (kRedRows * row_bytes);
-    if (group < 1) group = 1;
-    if (group > a.dy) group = a.dy;
-    const int64_t band = group * kRedRows * row_bytes;
-    if (band > 64 * 1024) {
-      xrs_set_error("xrs_affine: coarsen factor too large for one LDS band");
-      return XRS_ERR_ARG;
-    }
-    const int64_t nty = (a.out_h + kRedRows - 1) / kRedRows;
-    const int64_t ntx = (a.out_w + kTileW - 1) / kTileW;
-    const int64_t ntiles = ntx * nty * a.nt;
-    const int nb = grid_blocks(ntiles, 1, 256 * 16);
-    // stage capacity from the scale (+ taps, mirror and rounding margin); the
-    // kernel falls back to global taps for any tile whose span exceeds it
-    const char* stage_knob = std::getenv("XRS_AFFINE_STAGE");
-    // default off: staging without prefetch adds a dependent round trip per
-    // tile (config 3: 1.89 ms staged vs 0.90 ms direct, MI355X)
-    const bool use_stage = stage_knob && std::atoi(stage_knob) != 0;
-    if (use_stage) {  // per tile row / column block: source span of its taps
-      hipLaunchKernelGGL(affine_bounds_kernel, dim3(grid_blocks(nty + ntx, kThreads, 256)),
-                         dim3(kThreads), 0, st, ytab, xtab, ay.n, ax.n, kRedRows * a.dy,
-                         kTileW * a.dx, nty, ntx, yb, xb);
-      XRS_HIP_CHECK(hipGetLastError());
-    }
-    const int64_t rows_need = (int64_t)ceil((kRedRows * a.dy - 1) * fabs(ay.scale)) + 3;
-    const int64_t cols_need = (int64_t)ceil((kTileW * a.dx - 1) * fabs(ax.scale)) + 3;
-    const int64_t cap = rows_need * (cols_need + (cols_need - 1) / 32 + 1);
-    const bool two = ORDER == 1 && a.t_next != nullptr;
-    int64_t stage_bytes = ((cap * (int64_t)sizeof(T) * (two ? 2 : 1)) + 15) / 16 * 16;
-    int64_t stage_cap = cap;
-    if (!use_stage || stage_bytes + band > 64 * 1024) stage_bytes = stage_cap = 0;
-    const size_t lds = (size_t)(stage_bytes + band);
-    // sub-sample rows whose taps are loaded together (A/B knob XRS_AFFINE_BATCH)
-    const char* knob = std::getenv("XRS_AFFINE_BATCH");
-    const int kb = knob ? std::atoi(knob) : 2;
-    if (kb == 8)
-      hipLaunchKernelGGL((affine_reduce_kernel<T, I, ORDER, RECOVER, 8>), dim3(nb),
-                         dim3(kThreads), lds, st, args, ytab, xtab, (int)group, yb, xb,
-                         (int)stage_cap, (int)stage_bytes);
-    else if (kb == 2)
-      hipLaunchKernelGGL((affine_reduce_kernel<T, I, ORDER, RECOVER, 2>), dim3(nb),
-                         dim3(kThreads), lds, st, args, ytab, xtab, (int)group, yb, xb,
-                         (int)stage_cap, (int)stage_bytes);
-    else
-      hipLaunchKernelGGL((affine_reduce_kernel<T, I, ORDER, RECOVER, 4>), dim3(nb),
-                         dim3(kThreads), lds, st, args, ytab, xtab, (int)group, yb, xb,
-                         (int)stage_cap, (int)stage_bytes);
+    XRS_HIP_CHECK(hipGetLastError());
+    return XRS_OK;
   }
+  if (k3i) {
+    const int64_t ntiles = ((a.out_w + kThreads - 1) / kThreads) *
+                           ((a.out_h + kIntRows - 1) / kIntRows) * a.nt;
+    const int nb = grid_blocks(ntiles, 1, 1 << 24);
+    const int esz = (int)sizeof(T);
+    const int vb = (int)std::min<int64_t>(16, a.dx * esz);
+    const int vec_rows = ((uintptr_t)a.src % vb == 0) && ((a.src_sy * esz) % vb == 0) &&
+                         ((a.src_st * esz) % vb == 0);
+    if constexpr (std::is_floating_point<T>::value && std::is_same<T, I>::value && !RECOVER) {
+#define XRS_K3I(D)                                                                        \
+  if (a.dx == D)                                                                          \
+    hipLaunchKernelGGL((affine_reduce_integral_kernel<T, ORDER, D, D>), dim3(nb),         \
+                       dim3(kThreads), 0, st, args, ytab, xtab, vec_rows, nonint);
+      XRS_K3I(2) else XRS_K3I(4) else XRS_K3I(8)
+#undef XRS_K3I
+    }
+    XRS_HIP_CHECK(hipGetLastError());
+  }
+  const int64_t row_bytes = reduce_row_bytes(a.dx, sizeof(I));
+  int64_t group = kReduceLdsBudget / (kRedRows * row_bytes);
+  if (group < 1) group = 1;
+  if (group > a.dy) group = a.dy;
+  const int64_t band = group * kRedRows * row_bytes;
+  if (band > 64 * 1024) {
+    xrs_set_error("xrs_affine: coarsen factor too large for one LDS band");
+    return XRS_ERR_ARG;
+  }
+  const int64_t nty = (a.out_h + kRedRows - 1) / kRedRows;
+  const int64_t ntx = (a.out_w + kTileW - 1) / kTileW;
+  const int64_t ntiles = ntx * nty * a.nt;
+  // with K3i beside it, a small grid: it only reads the flag when K3i works
+  const int nb = grid_blocks(ntiles, 1, 256 * 16);
+  // stage capacity from the scale (+ taps, mirror and rounding margin); the
+  // kernel falls back to global taps for any tile whose span exceeds it
+  const char* stage_knob = std::getenv("XRS_AFFINE_STAGE");
+  // default off: staging without prefetch adds a dependent round trip per
+  // tile (config 3: 1.89 ms staged vs 0.90 ms direct, MI355X)
+  const bool use_stage = stage_knob && std::atoi(stage_knob) != 0;
+  if (use_stage) {  // per tile row / column block: source span of its taps
+    hipLaunchKernelGGL(affine_bounds_kernel, dim3(grid_blocks(nty + ntx, kThreads, 256)),
+                       dim3(kThreads), 0, st, ytab, xtab, ay.n, ax.n, kRedRows * a.dy,
+                       kTileW * a.dx, nty, ntx, yb, xb);
+    XRS_HIP_CHECK(hipGetLastError());
+  }
+  const int64_t rows_need = (int64_t)ceil((kRedRows * a.dy - 1) * fabs(ay.scale)) + 3;
+  const int64_t cols_need = (int64_t)ceil((kTileW * a.dx - 1) * fabs(ax.scale)) + 3;
+  const int64_t cap = rows_need * (cols_need + (cols_need - 1) / 32 + 1);
+  const bool two = ORDER == 1 && a.t_next != nullptr;
+  int64_t stage_bytes = ((cap * (int64_t)sizeof(T) * (two ? 2 : 1)) + 15) / 16 * 16;
+  int64_t stage_cap = cap;
+  if (!use_stage || stage_bytes + band > 64 * 1024) stage_bytes = stage_cap = 0;
+  const size_t lds = (size_t)(stage_bytes + band);
+  const int32_t* flag = k3i ? nonint : nullptr;
+  // sub-sample rows whose taps are loaded together (A/B knob XRS_AFFINE_BATCH)
+  const char* knob = std::getenv("XRS_AFFINE_BATCH");
+  const int kb = knob ? std::atoi(knob) : 2;
+  if (kb == 8)
+    hipLaunchKernelGGL((affine_reduce_kernel<T, I, ORDER, RECOVER, 8>), dim3(nb), dim3(kThreads),
+                       lds, st, args, ytab, xtab, (int)group, yb, xb, (int)stage_cap,
+                       (int)stage_bytes, flag);
+  else if (kb == 2)
+    hipLaunchKernelGGL((affine_reduce_kernel<T, I, ORDER, RECOVER, 2>), dim3(nb), dim3(kThreads),
+                       lds, st, args, ytab, xtab, (int)group, yb, xb, (int)stage_cap,
+                       (int)stage_bytes, flag);
+  else
+    hipLaunchKernelGGL((affine_reduce_kernel<T, I, ORDER, RECOVER, 4>), dim3(nb), dim3(kThreads),
+                       lds, st, args, ytab, xtab, (int)group, yb, xb, (int)stage_cap,
+                       (int)stage_bytes, flag);
   XRS_HIP_CHECK(hipGetLastError());
   return XRS_OK;
 }
@@ -680,8 +916,9 @@ extern "C" int xrs_any_nan(const void* src, int src_dtype, int64_t n, int32_t* f
 
 extern "C" int64_t xrs_affine_workspace_size(int64_t inter_h, int64_t inter_w) {
   if (inter_h < 0 || inter_w < 0) return 0;
-  // axis tables + per row / column block source spans (<= one per entry)
-  return (inter_h + inter_w) * (int64_t)(sizeof(xrs::AxisTab) + 2 * sizeof(int32_t));
+  // axis tables + per row / column block source spans (<= one per entry) +
+  // the K3i integrality flag
+  return (inter_h + inter_w) * (int64_t)(sizeof(xrs::AxisTab) + 2 * sizeof(int32_t)) + 16;
 }
 
 extern "C" int xrs_affine(const void* src, int src_dtype, int64_t nt, int64_t src_h,
@@ -730,15 +967,16 @@ extern "C" int xrs_affine(const void* src, int src_dtype, int64_t nt, int64_t sr
   AxisTab* xtab = ytab + ih;
   int32_t* yb = reinterpret_cast<int32_t*>(xtab + iw);
   int32_t* xb = yb + 2 * ih;
+  int32_t* nonint = xb + 2 * iw;
   hipStream_t st = static_cast<hipStream_t>(stream);
   return dispatch_dtype(src_dtype, [&](auto tag) -> int {
     using T = decltype(tag);
     if constexpr (std::is_floating_point<T>::value) {
       if (recover_nan)
-        return order ? launch<T, double, 1, true>(a, ay, ax, ytab, xtab, yb, xb, st)
-                     : launch<T, double, 0, true>(a, ay, ax, ytab, xtab, yb, xb, st);
+        return order ? launch<T, double, 1, true>(a, ay, ax, ytab, xtab, yb, xb, nonint, st)
+                     : launch<T, double, 0, true>(a, ay, ax, ytab, xtab, yb, xb, nonint, st);
     }
-    return order ? launch<T, T, 1, false>(a, ay, ax, ytab, xtab, yb, xb, st)
-                 : launch<T, T, 0, false>(a, ay, ax, ytab, xtab, yb, xb, st);
+    return order ? launch<T, T, 1, false>(a, ay, ax, ytab, xtab, yb, xb, nonint, st)
+                 : launch<T, T, 0, false>(a, ay, ax, ytab, xtab, yb, xb, nonint, st);
   });
 }

@@ -399,7 +399,7 @@ gather_separable_mlp_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t ba
 // the value is reused bit for bit instead of recomputed — one third fewer
 // float64 operations; the decisions are block-uniform (row entries are).
 // COND_LOADS additionally skips the loads of reused rows.
-template <typename T, typename O, int kRowsB, bool NT, bool COND_LOADS>
+template <typename T, typename O, int kRowsB, bool NT, bool COND_LOADS, int PX = kPx>
 __global__ void __launch_bounds__(kThreads)
 gather_bilinear_reuse_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t bands_per_tile,
                              int64_t segs_per_tile, int64_t nwork) {
@@ -411,10 +411,10 @@ gather_bilinear_reuse_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t b
     if (!work_item(g, w, ty0, nsegs, bands_per_tile, segs_per_tile, it)) continue;
     const AxisEntry* xt = a.xtab + it.t * g.tile_w + (it.c0 - it.tx * g.tile_w);
     const int ncols = (int)(it.c1 - it.c0);
-    int32_t cf[kPx], cc[kPx];
-    double dx[kPx];
+    int32_t cf[PX], cc[PX];
+    double dx[PX];
 #pragma unroll
-    for (int k = 0; k < kPx; ++k) {
+    for (int k = 0; k < PX; ++k) {
       const int lc = (int)threadIdx.x + k * kThreads;
       AxisEntry e{-1, -1, 0.0};
       if (lc < ncols) e = xt[lc];
@@ -428,13 +428,13 @@ gather_bilinear_reuse_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t b
       O* __restrict__ dst = static_cast<O*>(a.dst) + sn * a.dst_sn - g.row_begin * a.dst_sy + it.c0;
       // carried: source rows of the previous target row and their lerps
       int32_t pf = INT32_MIN, pc = INT32_MIN;
-      double ptop[kPx], pbot[kPx];
+      double ptop[PX], pbot[PX];
 #pragma unroll
-      for (int k = 0; k < kPx; ++k) ptop[k] = pbot[k] = 0.0;
+      for (int k = 0; k < PX; ++k) ptop[k] = pbot[k] = 0.0;
       for (int64_t r = it.r0; r < it.r1; r += kRowsB) {
         AxisEntry ye[kRowsB];
         bool need_f[kRowsB], need_c[kRowsB];
-        T v[kRowsB][4][kPx];
+        T v[kRowsB][4][PX];
         {
           int32_t qf = pf, qc = pc;
 #pragma unroll
@@ -453,14 +453,14 @@ gather_bilinear_reuse_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t b
           const T* rc = src + (int64_t)max(ye[q].c, 0) * a.src_sy;
           if (!COND_LOADS || need_f[q]) {
 #pragma unroll
-            for (int k = 0; k < kPx; ++k) {
+            for (int k = 0; k < PX; ++k) {
               v[q][0][k] = rf[max(cf[k], 0)];
               v[q][1][k] = rf[max(cc[k], 0)];
             }
           }
           if (!COND_LOADS || need_c[q]) {
 #pragma unroll
-            for (int k = 0; k < kPx; ++k) {
+            for (int k = 0; k < PX; ++k) {
               v[q][2][k] = rc[max(cf[k], 0)];
               v[q][3][k] = rc[max(cc[k], 0)];
             }
@@ -470,9 +470,9 @@ gather_bilinear_reuse_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t b
         for (int q = 0; q < kRowsB; ++q) {
           if (r + q >= it.r1) break;
           const bool okf = ye[q].f >= 0, okc = ye[q].c >= 0;
-          double top[kPx], bot[kPx];
+          double top[PX], bot[PX];
 #pragma unroll
-          for (int k = 0; k < kPx; ++k) {
+          for (int k = 0; k < PX; ++k) {
             const bool xf = cf[k] >= 0, xc = cc[k] >= 0;
             if (need_f[q]) {
               const T v00 = (okf && xf) ? v[q][0][k] : fill;
@@ -975,7 +975,7 @@ int launch(const GatherArgs& a, int coord_mode, AxisEntry* xtab, AxisEntry* ytab
   if (variant() == 14 && args.g.band > 64) args.g.band = 64;   // rows_s capacity
   const int64_t bands_per_tile = (g.tile_h + args.g.band - 1) / args.g.band;
   const int v = variant();
-  args.g.segw = kThreads * (v == 9 || v == 12 || v == 13 || v == 14 || v == 90 ? 2 : v == 10 ? 8 : v == 20 ? 4 : v == 11 ? 1 : kPx);
+  args.g.segw = kThreads * (v == 9 || v == 12 || v == 13 || v == 14 || v == 90 || v == 21 || v == 22 ? 2 : v == 10 ? 8 : v == 20 ? 4 : v == 11 ? 1 : kPx);
   const int64_t segs_per_tile = (g.tile_w + args.g.segw - 1) / args.g.segw;
   const int64_t nsegs = g.ntiles_x * segs_per_tile;
   const int64_t nwork = (ty1 - ty0) * bands_per_tile * nsegs;
@@ -1076,6 +1076,14 @@ int launch(const GatherArgs& a, int coord_mode, AxisEntry* xtab, AxisEntry* ytab
                            nwork, cap);
     } else if (v == 6 && INTERP == XRS_INTERP_BILINEAR)
       hipLaunchKernelGGL((gather_bilinear_reuse_kernel<T, O, 4, true, false>), dim3(nb),
+                         dim3(kThreads), 0, stream, args, ty0, nsegs, bands_per_tile,
+                         segs_per_tile, nwork);
+    else if (v == 21 && INTERP == XRS_INTERP_BILINEAR)
+      hipLaunchKernelGGL((gather_bilinear_reuse_kernel<T, O, 8, true, true, 2>), dim3(nb),
+                         dim3(kThreads), 0, stream, args, ty0, nsegs, bands_per_tile,
+                         segs_per_tile, nwork);
+    else if (v == 22 && INTERP == XRS_INTERP_BILINEAR)
+      hipLaunchKernelGGL((gather_bilinear_reuse_kernel<T, O, 4, true, true, 2>), dim3(nb),
                          dim3(kThreads), 0, stream, args, ty0, nsegs, bands_per_tile,
                          segs_per_tile, nwork);
     else if (v == 7 && INTERP == XRS_INTERP_BILINEAR)
