@@ -69,6 +69,7 @@ def _random_case(rng, dtype, nd, nan_frac):
         a.ravel()[rng.random(a.size) < nan_frac] = np.nan
         if nan_frac:
             a.ravel()[rng.integers(0, a.size)] = np.inf
+        a.ravel()[rng.integers(0, a.size, max(1, a.size // 50))] = -0.0   # order 0: -> +0.0
     else:
         a = rng.integers(0, 200, shp).astype(dtype)
     return a
@@ -144,11 +145,13 @@ def test_coarsen_via_dataset_api():
 @pytest.mark.parametrize("dtype,nd", [(np.float32, 2), (np.float64, 3), (np.float32, 3),
                                       (np.uint8, 2), (np.int16, 3)])
 @pytest.mark.parametrize("agg", ["mean", "sum", "max", "min", "count", "prod", "center"])
-def test_integral_grid_coarsen_special_values(dtype, nd, agg):
+@pytest.mark.parametrize("order", [1, 0])
+def test_integral_grid_coarsen_special_values(dtype, nd, agg, order):
     """Integer scales with integral offsets hit the kernel's exact shortcut for
     integral sample positions: NaN, +-inf and -0.0 around the taps (zero-weight
     neighbours included), the zero-weight time neighbour of 3-D inputs, and
-    chunk edges — engine == oracle bit for bit."""
+    chunk edges; order 0 too (scipy's order-0 value is 0.0 + v, so -0.0 comes
+    out as +0.0) — engine == oracle bit for bit."""
     import xcube_resampling_amd.affine as A
     from oracle import affine_ref
 
@@ -171,10 +174,11 @@ def test_integral_grid_coarsen_special_values(dtype, nd, agg):
                             (((2.0, 0.0, 2.0), (0.0, 3.0, -3.0)), (30, 38), (7, 16)),
                             (((1.0, 0.0, 1.0), (0.0, 1.0, 0.0)), (90, 76), (45, 76))]:
         ochunks = tuple(1 for _ in lead) + tile
-        ref = affine_ref.resample_array(a, m, lead + oshape, ochunks, 1, agg, False, fill)
-        got = A._resample_array(a, None, None, m, lead + oshape, ochunks, 1, agg, False, fill)
+        ref = affine_ref.resample_array(a, m, lead + oshape, ochunks, order, agg, False, fill)
+        got = A._resample_array(a, None, None, m, lead + oshape, ochunks, order, agg, False,
+                                fill)
         got = got if isinstance(got, np.ndarray) else got.cpu().numpy()
-        assert_bitwise_equal(got, np.asarray(ref), f"{dtype} {agg} {m}")
+        assert_bitwise_equal(got, np.asarray(ref), f"{dtype} {agg} order={order} {m}")
 
 
 @pytest.mark.parametrize("stage", ["0", "1"])

@@ -227,7 +227,10 @@ struct Taps {
       }
       return (I)ScipyOut<T>::cast(cval);
     }
-    if (ORDER == 0) return (I)v0[0][0];
+    if (ORDER == 0) {   // scipy's t = 0.0 + v*1.0: the value itself, -0 -> +0
+      const T a = v0[0][0];
+      return (I)(a == (T)0 ? (T)0 : a);
+    }
     if (!RECOVER && ey.w1 == 0.0 && ex.w1 == 0.0) {
       // Integral position (w0 = 1, w1 = 0 on both axes; every integer-factor
       // coarsen of aligned grids): scipy's sum below reduces EXACTLY to
@@ -604,7 +607,8 @@ affine_reduce_kernel(AffineArgs a, const AxisTab* __restrict__ ytab,
 // K3i: coarsen reducers when every sub-sample of a pixel sits on a source
 // pixel (scale 1 at the div-x grid with integral offsets — every aligned
 // integer-factor coarsen, config 3 — or any order-0 grid at scale 1).  A
-// sub-sample is then the source value itself (order 1: -0 -> +0, or NaN when
+// sub-sample is then the source value itself (-0 -> +0 as scipy's weighted sum
+// starting at 0.0 gives, order 1: NaN when
 // one of scipy's zero-weight taps is non-finite, see Taps::eval).  One thread
 // per output pixel, lanes on consecutive output columns: a sub-sample row is
 // one DX-wide vector load per lane (a wave reads 64*DX contiguous elements),
@@ -738,7 +742,7 @@ affine_reduce_integral_kernel(AffineArgs a, const AxisTab* __restrict__ ytab,
           for (int sj = 0; sj < DY; ++sj)
             fold.add_row(a.agg, DX, [&](int si) {
               const T x = v[sj][si];
-              return ORDER == 0 ? x : (x == (T)0 ? (T)0 : x);
+              return x == (T)0 ? (T)0 : x;   // scipy's t = 0.0 + w*x: -0 -> +0
             });
         }
       } else {
