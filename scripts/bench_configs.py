@@ -167,7 +167,8 @@ def config3(args):
         np.nan).size, args.cpu_seconds, 0)
     _line(3, "coarsen mean 4x4: 16384x16384 f32 -> 4096x4096 (affine bilinear at the 4x grid "
              "+ nanmean)", (n // k) ** 2, ms, wall, 4 * n * n + 4 * (n // k) ** 2,
-          "affine_kernel<float,float,1,false> (fused upscale+coarsen)",
+          "K3i affine_reduce_integral_kernel<float,1,4> (fused upscale+coarsen; edge pixels "
+          "via integral_slow_kernel)",
           dict(value=round(cpu_v, 3), unit="Mpixels/s", cores=1, kind="port",
                sample=f"{px // (cs // k) ** 2} passes of a 2048^2 -> 512^2 corner in {dt:.1f} s "
                       "(scipy affine_transform + numpy nanmean, dask chunk.coarsen order)"))

@@ -253,3 +253,34 @@ def test_integral_coarsen_k3i_matches_oracle(k3i, dtype, nd, monkeypatch):
         got = got if isinstance(got, np.ndarray) else got.cpu().numpy()
         assert_bitwise_equal(got, np.asarray(ref), f"k3i={k3i} {dtype} d={d} off={ox},{oy} "
                                                    f"order={order} {agg}")
+
+
+@pytest.mark.parametrize("nan_frac", [0.002, 0.05, 0.3])
+@pytest.mark.parametrize("order", [1, 0])
+def test_integral_coarsen_slow_list(nan_frac, order):
+    """K3i hands pixels with non-finite taps (order 1) or non-integral columns
+    to its slow-pixel list (exact path in integral_slow_kernel); a list longer
+    than the workspace holds (nan_frac 0.3, 3 slices) hands the whole launch to
+    the generic K3.  Every regime is bit-exact with the oracle."""
+    import xcube_resampling_amd.affine as A
+    from oracle import affine_ref
+
+    rng = np.random.default_rng(int(nan_frac * 1000) + order)
+    for dtype, d, lead in [(np.float32, 4, (3,)), (np.float64, 2, ()), (np.float32, 8, ())]:
+        oshape = (60, 70)
+        shp = lead + (oshape[0] * d + 2, oshape[1] * d + 5)
+        a = (rng.random(shp) * 4 - 2).astype(dtype)
+        flat = a.reshape(-1)
+        idx = rng.choice(flat.size, int(flat.size * nan_frac), replace=False)
+        flat[idx[: idx.size // 2]] = np.nan
+        flat[idx[idx.size // 2: 3 * idx.size // 4]] = np.inf
+        flat[idx[3 * idx.size // 4:]] = -0.0
+        m = ((float(d), 0.0, 0.0), (0.0, float(d), 0.0))
+        ochunks = tuple(1 for _ in lead) + (30, 70)
+        for agg in ("mean", "max"):
+            ref = affine_ref.resample_array(a, m, lead + oshape, ochunks, order, agg, False,
+                                            np.nan)
+            got = A._resample_array(a, None, None, m, lead + oshape, ochunks, order, agg, False,
+                                    np.nan)
+            got = got if isinstance(got, np.ndarray) else got.cpu().numpy()
+            assert_bitwise_equal(got, np.asarray(ref), f"{dtype} d={d} {agg} nan={nan_frac}")

@@ -100,14 +100,26 @@ __device__ inline bool integral_entry(const AxisTab& e, int32_t g_first, int k) 
          (ORDER == 0 || (e.w1 == 0.0 && e.g1 == e.g0 + 1));
 }
 
-// With `nonint` (K3i candidates, div dy x dx): also flag whether any in-bounds
-// entry breaks the integral-contiguous layout K3i's fast path needs (entry k of
+// With `nonint` (K3i candidates, div dy x dx): also count the in-bounds entries
+// that break the integral-contiguous layout K3i's fast path needs (entry k of
 // a pixel's run = first entry + k, order 1: weight 0 and the next tap at +1).
+// The image's last row / column (scipy mirrors the tap past it) always breaks
+// it; K3i serves such pixels through its exact path, so a few broken entries
+// still select K3i (`integral_limit`).
 template <int ORDER>
 __global__ void __launch_bounds__(kThreads)
 affine_tables_kernel(AxisChunks ay, AxisChunks ax, AxisTab* __restrict__ ytab,
                      AxisTab* __restrict__ xtab, int64_t dy, int64_t dx,
-                     int32_t* __restrict__ nonint) {
+                     int32_t* __restrict__ nonint, const int64_t* __restrict__ t_next,
+                     int64_t nt, int32_t* __restrict__ nonself) {
+  // K3i: does any slice have a zero-weight time neighbour other than itself?
+  if (nonself) {
+    bool other = false;
+    for (int64_t t = (int64_t)blockIdx.x * kThreads + threadIdx.x; t < nt;
+         t += (int64_t)gridDim.x * kThreads)
+      other = other || t_next[t] != t;
+    if (__any(other) && (threadIdx.x & 63) == 0) atomicOr(nonself, 1);
+  }
   const int64_t total = ay.n + ax.n;
   bool broken = false;
   for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < total;
@@ -123,7 +135,10 @@ affine_tables_kernel(AxisChunks ay, AxisChunks ax, AxisTab* __restrict__ ytab,
       broken = broken || f.g0 < 0 || !integral_entry<ORDER>(e, f.g0, (int)k);
     }
   }
-  if (nonint && __any(broken) && (threadIdx.x & 63) == 0) atomicOr(nonint, 1);
+  if (nonint) {   // count of broken entries (one atomic per wave)
+    const int nbroken = __popcll(__ballot(broken));
+    if (nbroken && (threadIdx.x & 63) == 0) atomicAdd(nonint, nbroken);
+  }
 }
 
 // ---- scipy output casts ----------------------------------------------------
@@ -493,8 +508,10 @@ __global__ void __launch_bounds__(kThreads)
 affine_reduce_kernel(AffineArgs a, const AxisTab* __restrict__ ytab,
                      const AxisTab* __restrict__ xtab, int group,
                      const int32_t* __restrict__ yb, const int32_t* __restrict__ xb,
-                     int stage_cap, int stage_bytes, const int32_t* __restrict__ nonint) {
-  if (nonint && !*nonint) return;   // K3i (launched before this one) did the work
+                     int stage_cap, int stage_bytes, const int32_t* __restrict__ nonint,
+                     int32_t nonint_limit, int64_t slow_cap) {
+  // K3i (launched before) did the work, unless its slow-pixel list overflowed
+  if (nonint && *nonint <= nonint_limit && nonint[2] <= slow_cap) return;
   extern __shared__ __align__(16) unsigned char smem[];
   T* stage0 = reinterpret_cast<T*>(smem);
   T* stage1 = stage0 + stage_cap;
@@ -607,47 +624,100 @@ affine_reduce_kernel(AffineArgs a, const AxisTab* __restrict__ ytab,
 // K3i: coarsen reducers when every sub-sample of a pixel sits on a source
 // pixel (scale 1 at the div-x grid with integral offsets — every aligned
 // integer-factor coarsen, config 3 — or any order-0 grid at scale 1).  A
-// sub-sample is then the source value itself (-0 -> +0 as scipy's weighted sum
-// starting at 0.0 gives, order 1: NaN when
-// one of scipy's zero-weight taps is non-finite, see Taps::eval).  One thread
-// per output pixel, lanes on consecutive output columns: a sub-sample row is
-// one DX-wide vector load per lane (a wave reads 64*DX contiguous elements),
-// the (DY+1) x (DX+1) source rect holding every tap of the pixel is loaded
-// once (the tap column right of the run comes from the next lane, the tap row
-// below is carried to the next output row).  Pixels whose table entries are
-// not integral-contiguous, or whose rect holds a non-finite value, take the
-// exact per-sub-sample path (Taps) — same result, slower.
-constexpr int kIntRows = 4;   // output rows per work item
+// sub-sample is then the source value itself, -0 -> +0 (scipy's weighted sum
+// starts at 0.0); order 1 adds zero-weight taps (the column right of the run,
+// the row below, the time neighbour) that only matter when non-finite (NaN).
+//
+// One thread per output pixel, lanes on consecutive output columns, a work
+// item = 256 output columns x R output rows.  When the item's R*D sub-sample
+// rows are one integral-contiguous run of source rows (everywhere but the
+// image's last row, where scipy mirrors the tap), every source row the item
+// needs is loaded up front — R*D (+1) DX-wide vector loads per lane, a wave
+// reads 64*D contiguous elements per row — so one memory round trip serves R
+// output rows.  The right tap column comes from the next lane.  A pixel whose
+// columns are not integral-contiguous, or whose rect holds a non-finite value
+// (order 1), is appended to a list that integral_slow_kernel evaluates
+// through the exact per-sub-sample path — same result, slower.  A list
+// longer than the workspace holds hands the whole launch to the generic K3.
+// output rows per item: 16 (f32) / 8 (f64) sub-sample rows of D elements
+inline constexpr int64_t int_rows(int64_t d, int64_t esz) {
+  return d >= 8 ? 1 : (16 / d) / (esz / 4) < 1 ? 1 : (16 / d) / (esz / 4);
+}
+template <typename T, int D> struct IntItem {
+  static constexpr int R = (int)int_rows(D, sizeof(T));
+};
 
+// DX consecutive elements; the compiler merges them into dwordx4 / dwordx2
+// loads (global loads need only element alignment on gfx950).  No run-time
+// alignment branch: a branch per row would serialise the item's loads.
 template <typename T, int DX>
-__device__ inline void load_run(const T* p, bool vec, T (&v)[DX]) {
-  constexpr int B = DX * (int)sizeof(T) >= 16 ? 16 : DX * (int)sizeof(T);
-  constexpr int PER = B / (int)sizeof(T);
-  typedef T V __attribute__((ext_vector_type(PER)));
-  if (vec) {
+__device__ inline void load_run(const T* p, T (&v)[DX]) {
 #pragma unroll
-    for (int c = 0; c < DX / PER; ++c) {
-      const V x = *reinterpret_cast<const V*>(p + c * PER);
-#pragma unroll
-      for (int e = 0; e < PER; ++e) v[c * PER + e] = x[e];
-    }
-  } else {
-#pragma unroll
-    for (int c = 0; c < DX; ++c) v[c] = p[c];
-  }
+  for (int c = 0; c < DX; ++c) v[c] = p[c];
 }
 
-template <typename T, int ORDER, int DY, int DX>
+// Exact path of one K3i pixel: every sub-sample through Taps (scipy's sum).
+template <typename T, int ORDER, int D>
+__device__ inline void integral_exact_pixel(
+    const T* g0, const T* g1, int64_t sy, bool two, const AxisTab* yrow, const AxisTab* xrun,
+    int agg, double cval, void* dst, int dst_dtype, int64_t didx) {
+  Src<T> p;
+  p.g0 = g0;
+  p.g1 = g1;
+  p.sy = sy;
+  AffineArgs a;   // only what Fold::store reads
+  a.agg = agg;
+  a.dst = dst;
+  a.dst_dtype = dst_dtype;
+  // table entries first, then one sub-sample row's taps at a time, all in
+  // flight together (D + 1 memory round trips instead of 2*D*D)
+  AxisTab ey[D], ex[D];
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    ey[k] = yrow[k];
+    ex[k] = xrun[k];
+  }
+  Fold<T> fold;
+#pragma unroll
+  for (int sj = 0; sj < D; ++sj) {
+    Taps<T> tp[D];
+    T sv[D];
+    if (ORDER == 1 && two) {
+#pragma unroll
+      for (int si = 0; si < D; ++si) tp[si].template load<ORDER, true>(p, ey[sj], ex[si]);
+#pragma unroll
+      for (int si = 0; si < D; ++si)
+        sv[si] = tp[si].template eval<T, ORDER, false, true>(ey[sj], ex[si], cval);
+    } else {
+#pragma unroll
+      for (int si = 0; si < D; ++si) tp[si].template load<ORDER, false>(p, ey[sj], ex[si]);
+#pragma unroll
+      for (int si = 0; si < D; ++si)
+        sv[si] = tp[si].template eval<T, ORDER, false, false>(ey[sj], ex[si], cval);
+    }
+    fold.add_row(agg, D, [&](int si) -> T { return sv[si]; });
+  }
+  fold.store(a, didx);
+}
+
+template <typename T, int ORDER, int D, bool TWO>
 __global__ void __launch_bounds__(kThreads)
 affine_reduce_integral_kernel(AffineArgs a, const AxisTab* __restrict__ ytab,
-                              const AxisTab* __restrict__ xtab, int vec_rows,
-                              const int32_t* __restrict__ nonint) {
-  if (*nonint) return;   // the generic K3 launched beside this one does the work
-  constexpr int NR = ORDER == 1 ? DY + 1 : DY;   // source rows of a pixel's rect
-  constexpr int B = DX * (int)sizeof(T) >= 16 ? 16 : DX * (int)sizeof(T);
+                              const AxisTab* __restrict__ xtab,
+                              const int32_t* __restrict__ nonint, int32_t nonint_limit,
+                              const int32_t* __restrict__ nonself, int32_t* __restrict__ nslow,
+                              int64_t* __restrict__ slow_list, int64_t slow_cap) {
+  if (*nonint > nonint_limit) return;   // the generic K3 launched beside this one works
+  // with time neighbours: the TWO=false instance serves launches where every
+  // neighbour is the slice itself (its taps are the ones already checked)
+  if (nonself && TWO != (*nonself != 0)) return;
+  constexpr int R = IntItem<T, D>::R;
+  constexpr int NE = R * D;                          // sub-sample rows of an item
+  constexpr int NRT = NE + (ORDER == 1 ? 1 : 0);     // source rows loaded
+  constexpr bool T1 = ORDER == 1 && TWO;
   const int lane = threadIdx.x & 63;
   const int64_t ntx = (a.out_w + kThreads - 1) / kThreads;
-  const int64_t nty = (a.out_h + kIntRows - 1) / kIntRows;
+  const int64_t nty = (a.out_h + R - 1) / R;
   const int64_t nwork = ntx * nty * a.nt;
   const XcdSlice sl = xcd_slice(nwork);
   for (int64_t w = sl.first; w < sl.end; w += sl.step) {
@@ -656,115 +726,138 @@ affine_reduce_integral_kernel(AffineArgs a, const AxisTab* __restrict__ ytab,
     const int64_t tj = rem / ntx, ti = rem - tj * ntx;
     const int64_t oi = ti * kThreads + threadIdx.x;
     const bool active = oi < a.out_w;
-    const int64_t t1 = a.t_next ? a.t_next[t] : -1;
-    const bool two = ORDER == 1 && t1 >= 0;
-    Src<T> p;
-    p.g0 = static_cast<const T*>(a.src) + t * a.src_st;
-    p.g1 = two ? static_cast<const T*>(a.src) + t1 * a.src_st : p.g0;
-    p.sy = a.src_sy;
+    const int64_t t1 = T1 ? a.t_next[t] : -1;
+    const T* g0 = static_cast<const T*>(a.src) + t * a.src_st;
+    const T* g1 = T1 && t1 >= 0 ? static_cast<const T*>(a.src) + t1 * a.src_st : g0;
 
-    // columns (row-invariant): the pixel's DX sub-sample columns must be one
-    // contiguous run of source columns c0 .. c0+DX-1
+    // columns: the pixel's D sub-sample columns must be one contiguous run
+    // c0 .. c0+D-1 (order 1: weight 0, right tap at +1)
+    // (entries loaded together, checked without short-circuit: one round trip)
+    AxisTab ex[D];
+    const int64_t ox = active ? oi : 0;
+#pragma unroll
+    for (int si = 0; si < D; ++si) ex[si] = xtab[ox * D + si];
+    const int32_t c0 = active ? ex[0].g0 : 0;
     bool col_fast = active;
-    int32_t c0 = 0;
-    if (active) {
-      const AxisTab e0 = xtab[oi * DX];
-      c0 = e0.g0;
 #pragma unroll
-      for (int si = 0; si < DX; ++si)
-        col_fast = col_fast && integral_entry<ORDER>(si ? xtab[oi * DX + si] : e0, c0, si);
-    }
-    const bool vec = vec_rows && ((int64_t)c0 * (int64_t)sizeof(T)) % B == 0;
-    // the tap column right of the run (order 1) from the next lane when that
-    // lane's run starts there
+    for (int si = 0; si < D; ++si) col_fast &= integral_entry<ORDER>(ex[si], c0, si);
+    // rows: lane l checks sub-sample row l of the item (wave-uniform result)
+    const int64_t oj0 = tj * R;
+    const int nrows = (int)min((int64_t)R, a.out_h - oj0);
+    const AxisTab* yitem = ytab + oj0 * D;
+    const AxisTab el = yitem[min(lane, nrows * D - 1)];
+    const int32_t gf = __builtin_amdgcn_readfirstlane(el.g0);   // lane 0's: scalar row math
+    const bool rows_fast =
+        nrows == R && __all(lane >= NE || (el.g0 >= 0 && el.g0 == gf + lane &&
+                                           (ORDER == 0 || (el.w1 == 0.0 && el.g1 == el.g0 + 1))));
+    const bool fast = rows_fast && col_fast;
+    // loads are unconditional (a branch per row would serialise them): lanes
+    // off the fast path read column 0 of the same rows and ignore the values
+    const int32_t cl = fast ? c0 : 0;
     const int32_t c0n = __shfl_down(c0, 1);
-    const bool fast_n = __shfl_down((int)col_fast, 1) != 0;
-    const bool nb_lane = lane < 63 && fast_n && c0n == c0 + DX;
+    const bool fast_n = __shfl_down((int)fast, 1) != 0;
+    const bool nb_lane = lane < 63 && fast_n && c0n == c0 + D;
+    const int32_t cnb = (fast && !nb_lane) ? c0 + D : cl;   // right tap column read here
 
-    int32_t carry = -1;   // source row carried from the previous output row
-    T cv[DX], cv1[DX], cnb = (T)0, cnb1 = (T)0;
-    const int64_t oj_end = min(a.out_h, (tj + 1) * kIntRows);
-    for (int64_t oj = tj * kIntRows; oj < oj_end; ++oj) {
-      const AxisTab* yrow = ytab + oj * DY;
-      const AxisTab ey0 = yrow[0];
-      bool row_fast = true;
+    T v[NRT][D], nbv[NRT], v1[T1 ? NRT : 1][T1 ? D : 1], nbv1[T1 ? NRT : 1];
+    if (rows_fast) {   // wave-uniform
 #pragma unroll
-      for (int sj = 0; sj < DY; ++sj)
-        row_fast = row_fast && integral_entry<ORDER>(sj ? yrow[sj] : ey0, ey0.g0, sj);
-      Fold<T> fold;
-      bool slow = !col_fast || !row_fast;
-      if (row_fast) {   // block-uniform
-        const int32_t r0 = ey0.g0;
-        T v[NR][DX], v1[NR][DX], nb[NR], nb1[NR];
-#pragma unroll
-        for (int r = 0; r < NR; ++r) {
-          if (ORDER == 1 && r == 0 && carry == r0) {
-#pragma unroll
-            for (int c = 0; c < DX; ++c) { v[0][c] = cv[c]; v1[0][c] = cv1[c]; }
-            nb[0] = cnb;
-            nb1[0] = cnb1;
-            continue;
-          }
-          if (col_fast) {   // other lanes take the exact path below
-            load_run<T, DX>(p.row0(r0 + r) + c0, vec, v[r]);
-            if (two) load_run<T, DX>(p.row1(r0 + r) + c0, vec, v1[r]);
-          }
-        }
-        if (ORDER == 1) {
-          bool bad = false;
-#pragma unroll
-          for (int r = 0; r < NR; ++r) {
-            if (!(ORDER == 1 && r == 0 && carry == r0)) {
-              const T sh = __shfl_down(v[r][0], 1);
-              nb[r] = nb_lane ? sh : (col_fast ? p.row0(r0 + r)[c0 + DX] : (T)0);
-              if (two) {
-                const T sh1 = __shfl_down(v1[r][0], 1);
-                nb1[r] = nb_lane ? sh1 : (col_fast ? p.row1(r0 + r)[c0 + DX] : (T)0);
-              }
-            }
-            bad = bad || !is_finite(nb[r]);
-            if (two) bad = bad || !is_finite(nb1[r]);
-#pragma unroll
-            for (int c = 0; c < DX; ++c) {
-              bad = bad || !is_finite(v[r][c]);
-              if (two) bad = bad || !is_finite(v1[r][c]);
-            }
-          }
-          slow = slow || bad;
-          carry = r0 + DY;
-#pragma unroll
-          for (int c = 0; c < DX; ++c) { cv[c] = v[DY][c]; cv1[c] = v1[DY][c]; }
-          cnb = nb[DY];
-          cnb1 = nb1[DY];
-        }
-        if (!slow) {
-#pragma unroll
-          for (int sj = 0; sj < DY; ++sj)
-            fold.add_row(a.agg, DX, [&](int si) {
-              const T x = v[sj][si];
-              return x == (T)0 ? (T)0 : x;   // scipy's t = 0.0 + w*x: -0 -> +0
-            });
-        }
-      } else {
-        carry = -1;
-      }
-      if (slow && active) {   // exact per-sub-sample evaluation (scipy's sum)
-        for (int sj = 0; sj < DY; ++sj) {
-          const AxisTab ey = yrow[sj];
-          fold.add_row(a.agg, DX, [&](int si) -> T {
-            const AxisTab ex = xtab[oi * DX + si];
-            Taps<T> tp;
-            if (two) {
-              tp.template load<ORDER, true>(p, ey, ex);
-              return tp.template eval<T, ORDER, false, true>(ey, ex, a.cval);
-            }
-            tp.template load<ORDER, false>(p, ey, ex);
-            return tp.template eval<T, ORDER, false, false>(ey, ex, a.cval);
-          });
+      for (int r = 0; r < NRT; ++r) {
+        const T* row = g0 + (int64_t)(gf + r) * a.src_sy;
+        load_run<T, D>(row + cl, v[r]);
+        if (ORDER == 1) nbv[r] = row[cnb];
+        if constexpr (T1) {
+          const T* row1 = g1 + (int64_t)(gf + r) * a.src_sy;
+          load_run<T, D>(row1 + cl, v1[r]);
+          nbv1[r] = row1[cnb];
         }
       }
-      if (active) fold.store(a, t * a.dst_st + oj * a.dst_sy + oi);
+      if (ORDER == 1) {
+#pragma unroll
+        for (int r = 0; r < NRT; ++r) {
+          const T sh = __shfl_down(v[r][0], 1);
+          nbv[r] = nb_lane ? sh : nbv[r];
+          if constexpr (T1) {
+            const T sh1 = __shfl_down(v1[r][0], 1);
+            nbv1[r] = nb_lane ? sh1 : nbv1[r];
+          }
+        }
+      }
     }
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+      if (q >= nrows) break;
+      const int64_t oj = oj0 + q;
+      const int64_t didx = t * a.dst_st + oj * a.dst_sy + oi;
+      bool slow = !fast;
+      if (ORDER == 1 && fast) {   // zero-weight taps: right column, row below, t+1
+#pragma unroll
+        for (int r = q * D; r <= q * D + D; ++r) {
+          slow = slow || !is_finite(nbv[r]);
+          if (T1) slow = slow || !is_finite(nbv1[T1 ? r : 0]);
+#pragma unroll
+          for (int c = 0; c < D; ++c) {
+            slow = slow || !is_finite(v[r][c]);
+            if (T1) slow = slow || !is_finite(v1[T1 ? r : 0][c]);
+          }
+        }
+      }
+      if (!active) continue;
+      if (slow) {   // the exact path runs in integral_slow_kernel (keeps its
+                    // registers out of this streaming kernel)
+        const int32_t k = atomicAdd(nslow, 1);
+        if (k < slow_cap) slow_list[k] = (t * a.out_h + oj) * a.out_w + oi;
+        continue;
+      }
+      auto sub = [&](int sj, int si) -> T {
+        const T x = v[q * D + sj][si];
+        return x == (T)0 ? (T)0 : x;   // scipy's 0.0 + w*x: -0 -> +0
+      };
+      if (a.agg == AGG_MEAN || a.agg == AGG_SUM) {   // the common case, lean
+        T total = (T)0;
+        int cnt = 0;
+#pragma unroll
+        for (int sj = 0; sj < D; ++sj)
+          total = total + pairwise_row<T>(D, [&](int si) {
+            const T x = sub(sj, si);
+            const bool nan = x != x;
+            cnt += nan ? 0 : 1;
+            return nan ? (T)0 : x;
+          });
+        const double res = a.agg == AGG_MEAN ? (double)(T)((double)total / (double)cnt)
+                                             : (double)total;
+        store_any(a.dst, didx, a.dst_dtype, res, 0, false);
+      } else {
+        Fold<T> fold;
+#pragma unroll
+        for (int sj = 0; sj < D; ++sj) fold.add_row(a.agg, D, [&](int si) { return sub(sj, si); });
+        fold.store(a, didx);
+      }
+    }
+  }
+}
+
+// K3i's slow pixels (exact path), one thread per listed pixel.  Runs only
+// when K3i worked and its list fit (else the generic K3 redid the launch).
+template <typename T, int ORDER, int D>
+__global__ void __launch_bounds__(kThreads)
+integral_slow_kernel(AffineArgs a, const AxisTab* __restrict__ ytab,
+                     const AxisTab* __restrict__ xtab, const int32_t* __restrict__ nonint,
+                     int32_t nonint_limit, const int64_t* __restrict__ slow_list,
+                     int64_t slow_cap) {
+  const int64_t n = nonint[2];
+  if (nonint[0] > nonint_limit || n > slow_cap) return;
+  for (int64_t k = (int64_t)blockIdx.x * kThreads + threadIdx.x; k < n;
+       k += (int64_t)gridDim.x * kThreads) {
+    const int64_t idx = slow_list[k];
+    const int64_t oi = idx % a.out_w, rest = idx / a.out_w;
+    const int64_t oj = rest % a.out_h, t = rest / a.out_h;
+    const T* g0 = static_cast<const T*>(a.src) + t * a.src_st;
+    const int64_t t1 = (ORDER == 1 && a.t_next) ? a.t_next[t] : -1;
+    const T* g1 = t1 >= 0 ? static_cast<const T*>(a.src) + t1 * a.src_st : g0;
+    integral_exact_pixel<T, ORDER, D>(g0, g1, a.src_sy, t1 >= 0, ytab + oj * D, xtab + oi * D,
+                                      a.agg, a.cval, a.dst, a.dst_dtype,
+                                      t * a.dst_st + oj * a.dst_sy + oi);
   }
 }
 
@@ -785,8 +878,18 @@ template <typename T, typename I, bool RECOVER>
 inline bool integral_candidate(const AffineArgs& a) {
   if (!std::is_floating_point<T>::value || !std::is_same<T, I>::value || RECOVER) return false;
   if (a.dx != a.dy || (a.dx != 2 && a.dx != 4 && a.dx != 8)) return false;
+  if (sizeof(T) == 8 && a.dx == 8) return false;   // 9 rows of 8 doubles: too many registers
   const char* knob = std::getenv("XRS_AFFINE_INTEGRAL");
   return !(knob && std::atoi(knob) == 0);
+}
+
+// Broken table entries K3i still takes (each costs its pixels the exact
+// path): the image edges plus a little; a grid off the integral layout (a
+// fractional offset) breaks nearly every entry and runs the generic K3.
+inline int64_t slow_capacity(int64_t ih, int64_t iw) { return 4 * (ih + iw) + 1024; }
+
+inline int32_t integral_limit(int64_t ih, int64_t iw) {
+  return (int32_t)std::min<int64_t>(INT32_MAX, 64 + (ih + iw) / 64);
 }
 
 template <typename T, typename I, int ORDER, bool RECOVER>
@@ -795,10 +898,17 @@ int launch(const AffineArgs& a, const AxisChunks& ay, const AxisChunks& ax, Axis
   const bool direct = a.agg == AGG_NONE || a.agg == AGG_FIRST || a.agg == AGG_LAST ||
                       a.agg == AGG_CENTER;
   const bool k3i = !direct && integral_candidate<T, I, RECOVER>(a);
-  if (k3i) XRS_HIP_CHECK(hipMemsetAsync(nonint, 0, sizeof(int32_t), st));
+  const int32_t limit = integral_limit(ay.n, ax.n);
+  // nonint[0]: broken entry count, nonint[1]: a time neighbour other than the slice
+  // nonint[2]: K3i's slow-pixel count (list of slow_cap entries after the flags)
+  const bool t1_flag = k3i && ORDER == 1 && a.t_next != nullptr;
+  if (k3i) XRS_HIP_CHECK(hipMemsetAsync(nonint, 0, 4 * sizeof(int32_t), st));
+  int64_t* slow_list = reinterpret_cast<int64_t*>(nonint + 4);
+  const int64_t slow_cap = slow_capacity(ay.n, ax.n);
   const int nbt = grid_blocks(ay.n + ax.n, kThreads, 1024);
   hipLaunchKernelGGL((affine_tables_kernel<ORDER>), dim3(nbt), dim3(kThreads), 0, st, ay, ax,
-                     ytab, xtab, a.dy, a.dx, k3i ? nonint : nullptr);
+                     ytab, xtab, a.dy, a.dx, k3i ? nonint : nullptr, a.t_next, a.nt,
+                     t1_flag ? nonint + 1 : nullptr);
   XRS_HIP_CHECK(hipGetLastError());
   AffineArgs args = a;
   args.ytab = ytab;
@@ -814,18 +924,25 @@ int launch(const AffineArgs& a, const AxisChunks& ay, const AxisChunks& ax, Axis
   }
   if (k3i) {
     const int64_t ntiles = ((a.out_w + kThreads - 1) / kThreads) *
-                           ((a.out_h + kIntRows - 1) / kIntRows) * a.nt;
+                           ((a.out_h + int_rows(a.dx, sizeof(T)) - 1) /
+                            int_rows(a.dx, sizeof(T))) * a.nt;
+    // one item per block (a persistent grid of 8 blocks per CU measured
+    // 266 vs 238 us at config 3)
     const int nb = grid_blocks(ntiles, 1, 1 << 24);
-    const int esz = (int)sizeof(T);
-    const int vb = (int)std::min<int64_t>(16, a.dx * esz);
-    const int vec_rows = ((uintptr_t)a.src % vb == 0) && ((a.src_sy * esz) % vb == 0) &&
-                         ((a.src_st * esz) % vb == 0);
     if constexpr (std::is_floating_point<T>::value && std::is_same<T, I>::value && !RECOVER) {
-#define XRS_K3I(D)                                                                        \
-  if (a.dx == D)                                                                          \
-    hipLaunchKernelGGL((affine_reduce_integral_kernel<T, ORDER, D, D>), dim3(nb),         \
-                       dim3(kThreads), 0, st, args, ytab, xtab, vec_rows, nonint);
-      XRS_K3I(2) else XRS_K3I(4) else XRS_K3I(8)
+#define XRS_K3I(D, TWO, SELF)                                                             \
+  hipLaunchKernelGGL((affine_reduce_integral_kernel<T, ORDER, D, TWO>), dim3(nb),         \
+                     dim3(kThreads), 0, st, args, ytab, xtab, nonint, limit, SELF,       \
+                     nonint + 2, slow_list, slow_cap)
+      // with time neighbours both instances launch; nonint[1] picks one
+      constexpr bool O1 = ORDER == 1;
+      int32_t* self = t1_flag ? nonint + 1 : nullptr;
+      if (a.dx == 2) { XRS_K3I(2, false, self); if (t1_flag) XRS_K3I(2, O1, self); }
+      else if (a.dx == 4) { XRS_K3I(4, false, self); if (t1_flag) XRS_K3I(4, O1, self); }
+      else if constexpr (sizeof(T) == 4) {
+        XRS_K3I(8, false, self);
+        if (t1_flag) XRS_K3I(8, O1, self);
+      }
 #undef XRS_K3I
     }
     XRS_HIP_CHECK(hipGetLastError());
@@ -871,16 +988,28 @@ int launch(const AffineArgs& a, const AxisChunks& ay, const AxisChunks& ax, Axis
   if (kb == 8)
     hipLaunchKernelGGL((affine_reduce_kernel<T, I, ORDER, RECOVER, 8>), dim3(nb), dim3(kThreads),
                        lds, st, args, ytab, xtab, (int)group, yb, xb, (int)stage_cap,
-                       (int)stage_bytes, flag);
+                       (int)stage_bytes, flag, limit, slow_cap);
   else if (kb == 2)
     hipLaunchKernelGGL((affine_reduce_kernel<T, I, ORDER, RECOVER, 2>), dim3(nb), dim3(kThreads),
                        lds, st, args, ytab, xtab, (int)group, yb, xb, (int)stage_cap,
-                       (int)stage_bytes, flag);
+                       (int)stage_bytes, flag, limit, slow_cap);
   else
     hipLaunchKernelGGL((affine_reduce_kernel<T, I, ORDER, RECOVER, 4>), dim3(nb), dim3(kThreads),
                        lds, st, args, ytab, xtab, (int)group, yb, xb, (int)stage_cap,
-                       (int)stage_bytes, flag);
+                       (int)stage_bytes, flag, limit, slow_cap);
   XRS_HIP_CHECK(hipGetLastError());
+  if (k3i) {
+    if constexpr (std::is_floating_point<T>::value && std::is_same<T, I>::value && !RECOVER) {
+#define XRS_K3S(D)                                                                        \
+  hipLaunchKernelGGL((integral_slow_kernel<T, ORDER, D>), dim3(256), dim3(kThreads), 0, st, \
+                     args, ytab, xtab, nonint, limit, slow_list, slow_cap)
+      if (a.dx == 2) XRS_K3S(2);
+      else if (a.dx == 4) XRS_K3S(4);
+      else if constexpr (sizeof(T) == 4) XRS_K3S(8);
+#undef XRS_K3S
+      XRS_HIP_CHECK(hipGetLastError());
+    }
+  }
   return XRS_OK;
 }
 
@@ -921,8 +1050,9 @@ extern "C" int xrs_any_nan(const void* src, int src_dtype, int64_t n, int32_t* f
 extern "C" int64_t xrs_affine_workspace_size(int64_t inter_h, int64_t inter_w) {
   if (inter_h < 0 || inter_w < 0) return 0;
   // axis tables + per row / column block source spans (<= one per entry) +
-  // the K3i integrality flag
-  return (inter_h + inter_w) * (int64_t)(sizeof(xrs::AxisTab) + 2 * sizeof(int32_t)) + 16;
+  // the K3i flags (broken entries, time neighbour, slow count) and slow-pixel list
+  return (inter_h + inter_w) * (int64_t)(sizeof(xrs::AxisTab) + 2 * sizeof(int32_t)) + 16 +
+         xrs::slow_capacity(inter_h, inter_w) * (int64_t)sizeof(int64_t);
 }
 
 extern "C" int xrs_affine(const void* src, int src_dtype, int64_t nt, int64_t src_h,
