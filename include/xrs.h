@@ -66,6 +66,20 @@ const char* xrs_version(void);
 const char* xrs_last_error(void);
 
 /* -------------------------------------------------------------------------
+ * Host-resident rasters (the reference's numpy-in / numpy-out contract,
+ * reproject.py:254-255, affine.py:227-228): page-lock a caller-owned host
+ * buffer in place so band-wise H2D / D2H copies run as DMA on their own
+ * streams, overlapped with the kernels (xcube_resampling_amd/streaming.py).
+ * xrs_host_register returns XRS_OK, or 1 when the range was already
+ * registered (the caller must then NOT unregister it), or XRS_ERR_HIP.
+ * ------------------------------------------------------------------------- */
+int xrs_host_register(void* ptr, int64_t bytes);
+int xrs_host_unregister(void* ptr);
+/* stream-ordered copy of `bytes` between any two of host / device memory
+ * (hipMemcpyAsync, direction from unified addressing) */
+int xrs_copy_async(void* dst, const void* src, int64_t bytes, void* stream);
+
+/* -------------------------------------------------------------------------
  * xrs_reproject — replaces `_reproject_block` (reproject.py:268-335) for ALL
  * target tiles of one variable in one launch, and the per-tile source-window
  * materialisation it depends on (`_reorganize_data_array_slice`,

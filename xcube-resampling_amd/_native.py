@@ -60,6 +60,9 @@ _c_ptr = ctypes.c_void_p
 _SIGNATURES = {
     "xrs_version": (ctypes.c_char_p, []),
     "xrs_last_error": (ctypes.c_char_p, []),
+    "xrs_host_register": (_c_int, [_c_ptr, _c_i64]),
+    "xrs_host_unregister": (_c_int, [_c_ptr]),
+    "xrs_copy_async": (_c_int, [_c_ptr, _c_ptr, _c_i64, _c_ptr]),
     "xrs_reproject": (_c_int, [
         _c_ptr, _c_int, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64,  # src
         _c_ptr, _c_int, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64,          # dst

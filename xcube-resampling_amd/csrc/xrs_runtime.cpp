@@ -3,6 +3,8 @@
 #include <cstdarg>
 #include <cstdio>
 
+#include <hip/hip_runtime.h>
+
 #include "../../include/xrs.h"
 
 namespace {
@@ -19,3 +21,51 @@ void xrs_set_error(const char* fmt, ...) {
 extern "C" const char* xrs_version(void) { return "xrs 0.1.0 (gfx950)"; }
 
 extern "C" const char* xrs_last_error(void) { return g_last_error; }
+
+extern "C" int xrs_host_register(void* ptr, int64_t bytes) {
+  if (!ptr || bytes <= 0) {
+    xrs_set_error("xrs_host_register: invalid argument");
+    return XRS_ERR_ARG;
+  }
+  const hipError_t e = hipHostRegister(ptr, (size_t)bytes, hipHostRegisterDefault);
+  if (e == hipErrorHostMemoryAlreadyRegistered) {
+    (void)hipGetLastError();
+    return 1;
+  }
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    xrs_set_error("hipHostRegister: %s", hipGetErrorString(e));
+    return XRS_ERR_HIP;
+  }
+  return XRS_OK;
+}
+
+extern "C" int xrs_host_unregister(void* ptr) {
+  if (!ptr) {
+    xrs_set_error("xrs_host_unregister: invalid argument");
+    return XRS_ERR_ARG;
+  }
+  const hipError_t e = hipHostUnregister(ptr);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    xrs_set_error("hipHostUnregister: %s", hipGetErrorString(e));
+    return XRS_ERR_HIP;
+  }
+  return XRS_OK;
+}
+
+extern "C" int xrs_copy_async(void* dst, const void* src, int64_t bytes, void* stream) {
+  if (!dst || !src || bytes < 0) {
+    xrs_set_error("xrs_copy_async: invalid argument");
+    return XRS_ERR_ARG;
+  }
+  if (bytes == 0) return XRS_OK;
+  const hipError_t e = hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyDefault,
+                                      static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    xrs_set_error("hipMemcpyAsync: %s", hipGetErrorString(e));
+    return XRS_ERR_HIP;
+  }
+  return XRS_OK;
+}

@@ -6,14 +6,21 @@
     reproject.py:326-328; dask's declared dtype is not enforced);
     "source" — store the float64 result in the (floating) source dtype, the
     dtype the reference *declares* (reproject.py:241): half the output bytes.
+
+``host_streaming_min_bytes``:
+    numpy (host-resident) sources at least this large are reprojected by the
+    band-wise H2D -> K1 -> D2H pipeline of ``streaming.reproject_host``
+    (page-locked in place, transfers overlapped with the kernels); smaller
+    ones are copied whole.  Default 64 MiB; 0 streams every host array.
 """
 
 from __future__ import annotations
 
 import contextlib
 
-_OPTIONS = {"reproject_bilinear_dtype": "float64"}
-_ALLOWED = {"reproject_bilinear_dtype": ("float64", "source")}
+_OPTIONS = {"reproject_bilinear_dtype": "float64", "host_streaming_min_bytes": 64 << 20}
+_ALLOWED = {"reproject_bilinear_dtype": ("float64", "source"),
+            "host_streaming_min_bytes": lambda v: isinstance(v, int) and v >= 0}
 
 
 def get_options() -> dict:
@@ -26,8 +33,9 @@ def set_options(**kwargs):
     for k, v in kwargs.items():
         if k not in _OPTIONS:
             raise KeyError(k)
-        if v not in _ALLOWED[k]:
-            raise ValueError(f"{k} must be one of {_ALLOWED[k]}")
+        allowed = _ALLOWED[k]
+        if not (allowed(v) if callable(allowed) else v in allowed):
+            raise ValueError(f"invalid value {v!r} for option {k}")
         _OPTIONS[k] = v
     try:
         yield

@@ -24,7 +24,7 @@ from dataclasses import dataclass, field
 
 import numpy as np
 
-from . import kernels
+from . import kernels, streaming
 from .constants import SCALE_LIMIT
 from .crs import Transformer
 from .dataset import DataArray, Dataset
@@ -228,20 +228,27 @@ def _reproject_data_array(data_array: DataArray, var_name, target_gm: GridMappin
     device = require_device()
     data = data_array.data
     on_device = is_device_array(data)
-    src = to_device(data, device)
-    expanded = src.dim() == 2
-    if expanded:
-        src = src.unsqueeze(0)
     out_dtype = None
     if interp_method == "bilinear" and get_options()["reproject_bilinear_dtype"] == "source":
         out_dtype = data_array.dtype if np.issubdtype(data_array.dtype, np.floating) else np.float64
-    out = kernels.reproject(src, plan, interp_method, fill_value, out_dtype=out_dtype)
+    expanded = len(data_array.dims) == 2
+    if not on_device and isinstance(data, np.ndarray) and \
+            data.nbytes >= get_options()["host_streaming_min_bytes"]:
+        # host array in, host array out (reproject.py:254-255): band pipeline
+        src = data.reshape((1,) + data.shape) if expanded else data
+        result = streaming.reproject_host(src, plan, interp_method, fill_value,
+                                          out_dtype=out_dtype, device=device)
+    else:
+        src = to_device(data, device)
+        if expanded:
+            src = src.unsqueeze(0)
+        out = kernels.reproject(src, plan, interp_method, fill_value, out_dtype=out_dtype)
+        result = out if on_device else out.cpu().numpy()
     if expanded:
-        out = out[0]
+        result = result[0]
         dims = (target_gm.xy_dim_names[1], target_gm.xy_dim_names[0])
     else:
         dims = (data_array.dims[0], target_gm.xy_dim_names[1], target_gm.xy_dim_names[0])
-    result = out if on_device else out.cpu().numpy()
     return DataArray(result, dims, data_array.attrs)
 
 
