@@ -507,6 +507,231 @@ gather_bilinear_reuse_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t b
   }
 }
 
+// ---- K1b-run (variant 23): 4 consecutive columns per lane, 8-element runs ----
+// At x scales near 1 (config 5: 0.994) pixel k of a lane's 4 consecutive
+// target columns has its floor column at cf[0] + k + {-1, 0, +1} and its ceil
+// column at floor + 1, so ONE run of 8 source elements starting at cf[0] - 1
+// holds every horizontal tap of the lane's 4 pixels: per source row two
+// 16-byte loads instead of 8 scalar gathers, per target row one 16-byte store
+// instead of 4.  Lanes whose columns do not fit (window / source edges,
+// exact-integer positions, other scales, a partial last lane) gather tap by
+// tap; the run loads stay unconditional (column 0 for such lanes) so no
+// branch separates the loads of a batch.
+template <typename T, typename O, int INTERP, int kRowsB>
+__global__ void __launch_bounds__(kThreads)
+gather_run_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t bands_per_tile,
+                  int64_t segs_per_tile, int64_t nwork, int vec_store) {
+  constexpr int RW = 8;
+  const Geometry& g = a.g;
+  const T fill = Conv<T>::from_f64(a.fill);
+  const XcdSlice sl = xcd_slice(nwork);
+  for (int64_t w = sl.first; w < sl.end; w += sl.step) {
+    WorkItem it;
+    if (!work_item(g, w, ty0, nsegs, bands_per_tile, segs_per_tile, it)) continue;
+    const AxisEntry* xt = a.xtab + it.t * g.tile_w + (it.c0 - it.tx * g.tile_w);
+    const int ncols = (int)(it.c1 - it.c0);
+    const int lc0 = 4 * (int)threadIdx.x;
+    int32_t cf[4], cc[4], sel[4];
+    double dx[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      AxisEntry e{-1, -1, 0.0};
+      if (lc0 + k < ncols) e = xt[lc0 + k];
+      cf[k] = e.f;
+      cc[k] = e.c;
+      dx[k] = e.d;
+    }
+    const int32_t ws = cf[0] - 1;
+    bool run = lc0 + 3 < ncols && ws >= 0 && (int64_t)ws + RW <= g.src_w;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      sel[k] = cf[k] - ws - k;   // run index of pixel k's floor tap, minus k: 0, 1 or 2
+      run = run && cf[k] >= 0 && cc[k] == cf[k] + 1 && sel[k] >= 0 && sel[k] <= 2;
+    }
+    const int32_t wsr = run ? ws : 0;
+    const bool vst = vec_store && lc0 + 3 < ncols;
+    const AxisEntry* yt = a.ytab + it.t * g.tile_h - it.ty * g.tile_h;
+    for (int64_t sn = 0; sn < a.n; ++sn) {
+      const T* __restrict__ src = static_cast<const T*>(a.src) + sn * a.src_sn;
+      O* __restrict__ dst =
+          static_cast<O*>(a.dst) + sn * a.dst_sn - g.row_begin * a.dst_sy + it.c0 + lc0;
+      for (int64_t r = it.r0; r < it.r1; r += kRowsB) {
+        AxisEntry ye[kRowsB];
+        T wf[kRowsB][RW], wc[kRowsB][RW];
+#pragma unroll
+        for (int q = 0; q < kRowsB; ++q) {
+          ye[q] = (r + q < it.r1) ? yt[r + q] : AxisEntry{-1, -1, 0.0};
+          const T* rf = src + (int64_t)max(ye[q].f, 0) * a.src_sy + wsr;
+          const T* rc = src + (int64_t)max(ye[q].c, 0) * a.src_sy + wsr;
+#pragma unroll
+          for (int e = 0; e < RW; ++e) {
+            wf[q][e] = rf[e];
+            wc[q][e] = rc[e];
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < kRowsB; ++q) {
+          if (r + q >= it.r1) break;
+          const bool okf = ye[q].f >= 0, okc = ye[q].c >= 0;
+          O out[4];
+          if (run) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              const int s = sel[k];
+              const T a0 = s == 0 ? wf[q][k] : (s == 1 ? wf[q][k + 1] : wf[q][k + 2]);
+              const T a1 = s == 0 ? wf[q][k + 1] : (s == 1 ? wf[q][k + 2] : wf[q][k + 3]);
+              const T b0 = s == 0 ? wc[q][k] : (s == 1 ? wc[q][k + 1] : wc[q][k + 2]);
+              const T b1 = s == 0 ? wc[q][k + 1] : (s == 1 ? wc[q][k + 2] : wc[q][k + 3]);
+              out[k] = Conv<O>::from_f64(interp4<T, INTERP>(okf ? a0 : fill, okf ? a1 : fill,
+                                                            okc ? b0 : fill, okc ? b1 : fill,
+                                                            dx[k], ye[q].d));
+            }
+          } else {   // tap by tap (edges)
+            const T* rf = src + (int64_t)max(ye[q].f, 0) * a.src_sy;
+            const T* rc = src + (int64_t)max(ye[q].c, 0) * a.src_sy;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              const bool xf = cf[k] >= 0, xc = cc[k] >= 0;
+              const int32_t f = max(cf[k], 0), c = max(cc[k], 0);
+              const T v00 = (okf && xf) ? rf[f] : fill;
+              const T v01 = (okf && xc) ? rf[c] : fill;
+              const T v10 = (okc && xf) ? rc[f] : fill;
+              const T v11 = (okc && xc) ? rc[c] : fill;
+              out[k] = Conv<O>::from_f64(interp4<T, INTERP>(v00, v01, v10, v11, dx[k], ye[q].d));
+            }
+          }
+          O* drow = dst + (r + q) * a.dst_sy;
+          if (vst) {
+            typedef O O2 __attribute__((ext_vector_type(2)));
+            if (sizeof(O) == 4) {
+              typedef O O4 __attribute__((ext_vector_type(4)));
+              const O4 o4 = {out[0], out[1], out[2], out[3]};
+              __builtin_nontemporal_store(o4, reinterpret_cast<O4*>(drow));
+            } else {
+              const O2 lo = {out[0], out[1]}, hi = {out[2], out[3]};
+              __builtin_nontemporal_store(lo, reinterpret_cast<O2*>(drow));
+              __builtin_nontemporal_store(hi, reinterpret_cast<O2*>(drow) + 1);
+            }
+          } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+              if (lc0 + k < ncols) __builtin_nontemporal_store(out[k], drow + k);
+          }
+        }
+      }
+    }
+  }
+}
+
+// ---- K1b-T (variant 24): variant-12 gathers, LDS-transposed 16-byte stores ----
+// Each wave owns 256 consecutive target columns; lane L gathers columns
+// L + 64k (k < 4: every tap load of the wave is 256 contiguous-ish bytes, as
+// in variant 12), then the wave transposes its row through a wave-private LDS
+// row (4 conflict-free dword writes, one ds_read_b128) so that lane L stores
+// columns 4L .. 4L+3 with ONE 16-byte non-temporal store instead of four
+// 4-byte ones.
+template <typename T, typename O, int INTERP, int kRowsB>
+__global__ void __launch_bounds__(kThreads)
+gather_transpose_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t bands_per_tile,
+                        int64_t segs_per_tile, int64_t nwork, int vec_store) {
+  __shared__ __align__(16) O lds[kThreads / 64][kRowsB][256];
+  const Geometry& g = a.g;
+  const T fill = Conv<T>::from_f64(a.fill);
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const XcdSlice sl = xcd_slice(nwork);
+  for (int64_t w = sl.first; w < sl.end; w += sl.step) {
+    WorkItem it;
+    if (!work_item(g, w, ty0, nsegs, bands_per_tile, segs_per_tile, it)) continue;
+    const int64_t wc0 = it.c0 + 256 * wv;   // this wave's first target column
+    const int ncols = (int)max((int64_t)0, min((int64_t)256, it.c1 - wc0));
+    if (ncols == 0) continue;
+    const AxisEntry* xt = a.xtab + it.t * g.tile_w + (wc0 - it.tx * g.tile_w);
+    int32_t cf[4], cc[4];
+    double dx[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int lc = lane + 64 * k;
+      AxisEntry e{-1, -1, 0.0};
+      if (lc < ncols) e = xt[lc];
+      cf[k] = e.f;
+      cc[k] = e.c;
+      dx[k] = e.d;
+    }
+    const bool vst = vec_store && 4 * lane + 3 < ncols;
+    const AxisEntry* yt = a.ytab + it.t * g.tile_h - it.ty * g.tile_h;
+    for (int64_t sn = 0; sn < a.n; ++sn) {
+      const T* __restrict__ src = static_cast<const T*>(a.src) + sn * a.src_sn;
+      O* __restrict__ dst = static_cast<O*>(a.dst) + sn * a.dst_sn - g.row_begin * a.dst_sy + wc0;
+      for (int64_t r = it.r0; r < it.r1; r += kRowsB) {
+        AxisEntry ye[kRowsB];
+        T v[kRowsB][4][4];
+#pragma unroll
+        for (int q = 0; q < kRowsB; ++q) {
+          ye[q] = (r + q < it.r1) ? yt[r + q] : AxisEntry{-1, -1, 0.0};
+          const T* rf = src + (int64_t)max(ye[q].f, 0) * a.src_sy;
+          const T* rc = src + (int64_t)max(ye[q].c, 0) * a.src_sy;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int32_t f = max(cf[k], 0), c = max(cc[k], 0);
+            v[q][0][k] = rf[f];
+            if (INTERP != XRS_INTERP_NEAREST) {
+              v[q][1][k] = rf[c];
+              v[q][2][k] = rc[f];
+              v[q][3][k] = rc[c];
+            }
+          }
+        }
+        // the previous batch's LDS reads are done before this batch's writes
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+#pragma unroll
+        for (int q = 0; q < kRowsB; ++q) {
+          const bool okf = ye[q].f >= 0, okc = ye[q].c >= 0;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const bool xf = cf[k] >= 0, xc = cc[k] >= 0;
+            const T v00 = (okf && xf) ? v[q][0][k] : fill;
+            O out;
+            if (INTERP == XRS_INTERP_NEAREST) {
+              out = (O)v00;
+            } else {
+              const T v01 = (okf && xc) ? v[q][1][k] : fill;
+              const T v10 = (okc && xf) ? v[q][2][k] : fill;
+              const T v11 = (okc && xc) ? v[q][3][k] : fill;
+              out = Conv<O>::from_f64(interp4<T, INTERP>(v00, v01, v10, v11, dx[k], ye[q].d));
+            }
+            lds[wv][q][lane + 64 * k] = out;
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+#pragma unroll
+        for (int q = 0; q < kRowsB; ++q) {
+          if (r + q >= it.r1) break;
+          O* drow = dst + (r + q) * a.dst_sy;
+          if (vst) {
+            typedef O O2 __attribute__((ext_vector_type(2)));
+            if (sizeof(O) == 4) {
+              typedef O O4 __attribute__((ext_vector_type(4)));
+              const O4 o4 = *reinterpret_cast<const O4*>(&lds[wv][q][4 * lane]);
+              __builtin_nontemporal_store(o4, reinterpret_cast<O4*>(drow + 4 * lane));
+            } else {
+              const O2 lo = *reinterpret_cast<const O2*>(&lds[wv][q][4 * lane]);
+              const O2 hi = *reinterpret_cast<const O2*>(&lds[wv][q][4 * lane + 2]);
+              __builtin_nontemporal_store(lo, reinterpret_cast<O2*>(drow + 4 * lane));
+              __builtin_nontemporal_store(hi, reinterpret_cast<O2*>(drow + 4 * lane) + 1);
+            }
+          } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+              if (4 * lane + k < ncols)
+                __builtin_nontemporal_store(lds[wv][q][4 * lane + k], drow + 4 * lane + k);
+          }
+        }
+      }
+    }
+  }
+}
+
 // ---- K1c: per-pixel gather (2-D coordinate tables) --------------------------
 template <typename T, typename O, int INTERP>
 __global__ void __launch_bounds__(kThreads)
@@ -959,6 +1184,13 @@ gather_wave_staged_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t band
 //          of 4 target rows, one 16-byte store per lane and row: 3.48 ms
 //          (12: 2.56 ms) — the LDS round trip and 168 VGPRs cost more than the
 //          saved gathers; lane-strided pixels with dword stores: 3.85 ms.
+//   23     4 consecutive columns per lane, taps from one 8-element run per
+//          source row (two 16-byte loads) and 16-byte stores: 2.97 ms vs 2.66
+//          (8192^2: 0.145 vs 0.110 ms) — fewer, wider memory instructions do
+//          not pay: K1 is not VMEM-issue bound
+//   24     variant-12 gathers (4 rows x 4 columns per lane) with the output
+//          row transposed through LDS into 16-byte stores: 2.88 vs 2.66 ms
+//          (8192^2: 0.125 vs 0.110) — the dword stores are not the limit either
 inline int variant() {
   const char* v = getenv("XRS_REPROJECT_VARIANT");
   return v ? atoi(v) : 12;
@@ -975,7 +1207,7 @@ int launch(const GatherArgs& a, int coord_mode, AxisEntry* xtab, AxisEntry* ytab
   if (variant() == 14 && args.g.band > 64) args.g.band = 64;   // rows_s capacity
   const int64_t bands_per_tile = (g.tile_h + args.g.band - 1) / args.g.band;
   const int v = variant();
-  args.g.segw = kThreads * (v == 9 || v == 12 || v == 13 || v == 14 || v == 90 || v == 21 || v == 22 ? 2 : v == 10 ? 8 : v == 20 ? 4 : v == 11 ? 1 : kPx);
+  args.g.segw = kThreads * (v == 9 || v == 12 || v == 13 || v == 14 || v == 90 || v == 21 || v == 22 ? 2 : v == 10 ? 8 : (v == 20 || v == 23 || v == 24) ? 4 : v == 11 ? 1 : kPx);
   const int64_t segs_per_tile = (g.tile_w + args.g.segw - 1) / args.g.segw;
   const int64_t nsegs = g.ntiles_x * segs_per_tile;
   const int64_t nwork = (ty1 - ty0) * bands_per_tile * nsegs;
@@ -1078,7 +1310,22 @@ int launch(const GatherArgs& a, int coord_mode, AxisEntry* xtab, AxisEntry* ytab
       hipLaunchKernelGGL((gather_bilinear_reuse_kernel<T, O, 4, true, false>), dim3(nb),
                          dim3(kThreads), 0, stream, args, ty0, nsegs, bands_per_tile,
                          segs_per_tile, nwork);
-    else if (v == 21 && INTERP == XRS_INTERP_BILINEAR)
+    else if ((v == 23 || v == 24) && std::is_same<T, float>::value) {
+      // 16-byte output stores need 4-element aligned output runs
+      const bool vst = ((uintptr_t)a.dst % (4 * sizeof(O)) == 0 || sizeof(O) == 8) &&
+                       ((uintptr_t)a.dst % 16 == 0) && (a.dst_sy % 4 == 0) &&
+                       (a.dst_sn % 4 == 0) && (g.tile_w % 4 == 0);
+      if constexpr (std::is_same<T, float>::value) {
+        if (v == 23 && INTERP != XRS_INTERP_NEAREST)
+          hipLaunchKernelGGL((gather_run_kernel<T, O, INTERP, 4>), dim3(nb), dim3(kThreads), 0,
+                             stream, args, ty0, nsegs, bands_per_tile, segs_per_tile, nwork,
+                             (int)vst);
+        else
+          hipLaunchKernelGGL((gather_transpose_kernel<T, O, INTERP, 4>), dim3(nb),
+                             dim3(kThreads), 0, stream, args, ty0, nsegs, bands_per_tile,
+                             segs_per_tile, nwork, (int)vst);
+      }
+    } else if (v == 21 && INTERP == XRS_INTERP_BILINEAR)
       hipLaunchKernelGGL((gather_bilinear_reuse_kernel<T, O, 8, true, true, 2>), dim3(nb),
                          dim3(kThreads), 0, stream, args, ty0, nsegs, bands_per_tile,
                          segs_per_tile, nwork);
