@@ -152,11 +152,18 @@ def main():
     from xcube_resampling_amd.sharding import band_shard, env_rank, max_over_ranks
 
     rank, world, local_rank = env_rank()
-    torch.cuda.set_device(local_rank)
-    device = torch.device("cuda", local_rank)
+    # one GPU per rank; XRS_BENCH_BACKEND=gloo with more ranks than GPUs is only
+    # a rehearsal of the multi-rank logic on a smaller box (ranks share GPUs)
+    backend = os.environ.get("XRS_BENCH_BACKEND", "nccl")
+    dev_index = local_rank % torch.cuda.device_count() if backend == "gloo" else local_rank
+    torch.cuda.set_device(dev_index)
+    device = torch.device("cuda", dev_index)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=device)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group(backend)
 
     src_gm, tgm, plan, lon, lat = workload(args.size, args.tile)
     out_np = np.float32 if args.out_dtype == "f32" else np.float64
@@ -183,7 +190,10 @@ def main():
 
     def barrier():
         if world > 1:
-            dist.barrier(device_ids=[local_rank])
+            if backend == "nccl":
+                dist.barrier(device_ids=[dev_index])
+            else:
+                dist.barrier()
 
     barrier()
     torch.cuda.synchronize()

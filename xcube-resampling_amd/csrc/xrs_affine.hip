@@ -21,7 +21,9 @@
 //   sub-sample): one output pixel per thread, lanes on consecutive columns,
 //   scipy's corner sum ((v*wy)*wx accumulated from +0.0 in corner order, last
 //   dim fastest; the zero-weight time neighbour of order-1 3-D transforms
-//   included, as it propagates NaN) evaluated from global memory.
+//   included, as it propagates NaN) evaluated from global memory.  Its two
+//   table entries are evaluated inline (the same axis_entry), so plain
+//   affine is ONE launch (config 1 is launch-latency bound).
 // K3 affine_reduce_kernel (mean/sum/max/min/prod/count): per 64x4 output
 //   tile, the intermediate band of a group of sub-sample rows is evaluated
 //   into LDS with lanes on consecutive intermediate columns (coalesced), then
@@ -321,8 +323,7 @@ __device__ inline int32_t wave_uniform(int32_t v) { return __builtin_amdgcn_read
 // near 1 — source reads), the row entry wave-uniform (scalar loads).
 template <typename T, typename I, int ORDER, bool RECOVER>
 __global__ void __launch_bounds__(kThreads)
-affine_direct_kernel(AffineArgs a, const AxisTab* __restrict__ ytab,
-                     const AxisTab* __restrict__ xtab) {
+affine_direct_kernel(AffineArgs a, AxisChunks ay, AxisChunks ax) {
   const int tx = threadIdx.x % kTileW;
   const int ty = wave_uniform(threadIdx.x / kTileW);
   const int64_t ntx = (a.out_w + kTileW - 1) / kTileW, nty = (a.out_h + kTileH - 1) / kTileH;
@@ -342,9 +343,9 @@ affine_direct_kernel(AffineArgs a, const AxisTab* __restrict__ ytab,
     p.g0 = static_cast<const T*>(a.src) + t * a.src_st;
     p.g1 = t1 >= 0 ? static_cast<const T*>(a.src) + t1 * a.src_st : p.g0;
     p.sy = a.src_sy;
-    const AxisTab ey = ytab[oj * a.dy + sj];
+    const AxisTab ey = axis_entry<ORDER>(ay, oj * a.dy + sj);   // wave-uniform
     if (oi < a.out_w) {
-      const AxisTab ex = xtab[oi * a.dx + si];
+      const AxisTab ex = axis_entry<ORDER>(ax, oi * a.dx + si);
       I v;
       if (ORDER == 1 && t1 >= 0) v = subsample<T, I, ORDER, RECOVER, true>(p, ey, ex, a.cval);
       else v = subsample<T, I, ORDER, RECOVER, false>(p, ey, ex, a.cval);
@@ -905,23 +906,23 @@ int launch(const AffineArgs& a, const AxisChunks& ay, const AxisChunks& ax, Axis
   if (k3i) XRS_HIP_CHECK(hipMemsetAsync(nonint, 0, 4 * sizeof(int32_t), st));
   int64_t* slow_list = reinterpret_cast<int64_t*>(nonint + 4);
   const int64_t slow_cap = slow_capacity(ay.n, ax.n);
+  AffineArgs args = a;
+  args.ytab = ytab;
+  args.xtab = xtab;
+  if (direct) {   // one launch: the kernel evaluates its two table entries inline
+    const int64_t ntiles =
+        ((a.out_w + kTileW - 1) / kTileW) * ((a.out_h + kTileH - 1) / kTileH) * a.nt;
+    const int nb = grid_blocks(ntiles, 1, 256 * 64);
+    hipLaunchKernelGGL((affine_direct_kernel<T, I, ORDER, RECOVER>), dim3(nb), dim3(kThreads), 0,
+                       st, args, ay, ax);
+    XRS_HIP_CHECK(hipGetLastError());
+    return XRS_OK;
+  }
   const int nbt = grid_blocks(ay.n + ax.n, kThreads, 1024);
   hipLaunchKernelGGL((affine_tables_kernel<ORDER>), dim3(nbt), dim3(kThreads), 0, st, ay, ax,
                      ytab, xtab, a.dy, a.dx, k3i ? nonint : nullptr, a.t_next, a.nt,
                      t1_flag ? nonint + 1 : nullptr);
   XRS_HIP_CHECK(hipGetLastError());
-  AffineArgs args = a;
-  args.ytab = ytab;
-  args.xtab = xtab;
-  if (direct) {
-    const int64_t ntiles =
-        ((a.out_w + kTileW - 1) / kTileW) * ((a.out_h + kTileH - 1) / kTileH) * a.nt;
-    const int nb = grid_blocks(ntiles, 1, 256 * 64);
-    hipLaunchKernelGGL((affine_direct_kernel<T, I, ORDER, RECOVER>), dim3(nb), dim3(kThreads), 0,
-                       st, args, ytab, xtab);
-    XRS_HIP_CHECK(hipGetLastError());
-    return XRS_OK;
-  }
   if (k3i) {
     const int64_t ntiles = ((a.out_w + kThreads - 1) / kThreads) *
                            ((a.out_h + int_rows(a.dx, sizeof(T)) - 1) /
