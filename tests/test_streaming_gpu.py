@@ -92,3 +92,39 @@ def test_streamed_errors():
         streaming.reproject_host(g["data"], plan, "cubic", np.nan)
     with pytest.raises(ValueError, match="does not match the plan"):
         streaming.reproject_host(g["data"][:, :-1], plan, "nearest", np.nan)
+
+
+def test_pinned_transfers_in_affine_and_rectify_paths():
+    """The dataset APIs move numpy arrays of at least host_streaming_min_bytes
+    by DMA from page-locked memory (streaming.host_to_device / device_to_host):
+    same bits as the small-array path."""
+    import xcube_resampling_amd as xrs
+
+    rng = np.random.default_rng(5)
+    # affine (coarsen 4x4 mean, 3-D) on a regular EPSG:4326 grid
+    n = 256
+    res = 2.0 ** -8
+    lon = (np.arange(n) + 0.5) * res
+    lat = n * res - (np.arange(n) + 0.5) * res
+    data = rng.random((2, n, n), dtype=np.float32)
+    data.ravel()[rng.choice(data.size, 100, replace=False)] = np.nan
+    ds = xrs.Dataset(data_vars={"v": (("t", "lat", "lon"), data)},
+                     coords={"lon": ("lon", lon), "lat": ("lat", lat)})
+    tgm = xrs.GridMapping.regular((n // 4, n // 4), (0, 0), res * 4, "EPSG:4326")
+    # irregular swath for rectify
+    h, w = 120, 100
+    ii, jj = np.meshgrid(np.arange(w), np.arange(h))
+    slat = 60 - 0.0027 * jj - 0.0004 * ii
+    slon = 5 + 0.0045 * ii + 0.0009 * jj
+    sds = xrs.Dataset(data_vars={"v": (("y", "x"), rng.random((h, w), dtype=np.float32))},
+                      coords={"lon": (("y", "x"), slon), "lat": (("y", "x"), slat)})
+    results = []
+    for min_bytes in (1 << 40, 0):
+        with xrs.set_options(host_streaming_min_bytes=min_bytes):
+            a = xrs.affine_transform_dataset(ds, tgm, agg_methods="mean")["v"].values
+            r = xrs.rectify_dataset(sds, interp_methods="bilinear")["v"].values
+        assert isinstance(a, np.ndarray) and isinstance(r, np.ndarray)
+        results.append((a, r))
+    assert_bitwise_equal(results[1][0], results[0][0], "affine")
+    assert_bitwise_equal(results[1][1], results[0][1], "rectify")
+    assert np.isfinite(results[0][1]).sum() > h * w // 2

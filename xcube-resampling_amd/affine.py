@@ -21,6 +21,7 @@ import numpy as np
 from . import _native, kernels
 from .dataset import DataArray, Dataset
 from .device import is_device_array, require_device, to_device
+from .streaming import device_to_host, host_to_device
 from .gridmapping import GridMapping
 from .utils import (
     _can_apply_affine_transform,
@@ -286,7 +287,7 @@ def _resample_array(data, dims, chunks, affine_matrix, output_shape, output_chun
     if len(data.shape) > 3:
         raise NotImplementedError("the engine resamples 2-D and 3-D variables")
     device = require_device()
-    src = to_device(data, device)
+    src = host_to_device(data, device)
     expanded = src.dim() == 2
     if expanded:
         src = src.unsqueeze(0)
@@ -331,7 +332,7 @@ def resample_dataset(dataset, affine_matrix, yx_dims: tuple[str, str], target_si
                 _get_recover_nan(recover_nans, var_name, data_array),
                 _get_fill_value(fill_values, var_name, data_array))
             if not on_device and not isinstance(res, np.ndarray):
-                res = res.cpu().numpy()
+                res = device_to_host(res)
             new = DataArray(res, data_array.dims, data_array.attrs)
         elif yx_dims[0] not in data_array.dims and yx_dims[1] not in data_array.dims:
             new = data_array

@@ -902,7 +902,8 @@ int launch(const AffineArgs& a, const AxisChunks& ay, const AxisChunks& ax, Axis
   const int32_t limit = integral_limit(ay.n, ax.n);
   // nonint[0]: broken entry count, nonint[1]: a time neighbour other than the slice
   // nonint[2]: K3i's slow-pixel count (list of slow_cap entries after the flags)
-  const bool t1_flag = k3i && ORDER == 1 && a.t_next != nullptr;
+  // (one slice: its only possible neighbour is itself -> the TWO=false instance)
+  const bool t1_flag = k3i && ORDER == 1 && a.t_next != nullptr && a.nt > 1;
   if (k3i) XRS_HIP_CHECK(hipMemsetAsync(nonint, 0, 4 * sizeof(int32_t), st));
   int64_t* slow_list = reinterpret_cast<int64_t*>(nonint + 4);
   const int64_t slow_cap = slow_capacity(ay.n, ax.n);

@@ -29,6 +29,7 @@ from .constants import SCALE_LIMIT, UV_DELTA
 from .crs import Transformer
 from .dataset import DataArray, Dataset
 from .device import is_device_array, require_device, to_device
+from .streaming import device_to_host, host_to_device
 from .gridmapping import GridMapping
 from .gridmapping.helpers import chunk_sizes
 from .utils import (
@@ -164,7 +165,7 @@ def _compute_target_source_ij(source_gm: GridMapping, target_gm: GridMapping,
     source coordinates are uploaded once and shared by K4 and K5."""
     device = require_device()
     xy = source_gm.xy_coords.data
-    xy = (to_device(xy[0], device, np.float64), to_device(xy[1], device, np.float64))
+    xy = (host_to_device(xy[0], device, np.float64), host_to_device(xy[1], device, np.float64))
     dst_y_scale = target_gm.y_res if target_gm.is_j_axis_up else -target_gm.y_res
     tiles = _device_tiles(source_gm, target_gm, xy)
     if tiles is None:   # boxes not a regular tile grid: host tiling
@@ -197,7 +198,7 @@ def _rectify_data_array(data_array: DataArray, var_name, target_gm: GridMapping,
     interp_method = _get_interp_method_str(interp_methods, var_name, data_array)
     device = require_device()
     on_device = is_device_array(data_array.data)
-    src = to_device(data_array.data, device)
+    src = host_to_device(data_array.data, device)
     expanded = src.dim() == 2
     if expanded:
         src = src.unsqueeze(0)
@@ -207,4 +208,4 @@ def _rectify_data_array(data_array: DataArray, var_name, target_gm: GridMapping,
         dims = (target_gm.xy_dim_names[1], target_gm.xy_dim_names[0])
     else:
         dims = (data_array.dims[0], target_gm.xy_dim_names[1], target_gm.xy_dim_names[0])
-    return DataArray(out if on_device else out.cpu().numpy(), dims, data_array.attrs)
+    return DataArray(out if on_device else device_to_host(out), dims, data_array.attrs)

@@ -24,7 +24,8 @@ import ctypes
 import numpy as np
 
 from . import _native, kernels
-from .device import empty, require_device, stream_handle, torch
+from .device import empty, numpy_dtype, require_device, stream_handle, to_device, torch
+from .options import get_options
 
 
 class HostPin:
@@ -58,6 +59,43 @@ def _copy(dst_ptr: int, src_ptr: int, nbytes: int, stream) -> None:
     rc = _native.lib().xrs_copy_async(ctypes.c_void_p(dst_ptr), ctypes.c_void_p(src_ptr),
                                       int(nbytes), stream_handle(stream=stream))
     _native.check(rc, "xrs_copy_async")
+
+
+def host_to_device(arr, device, dtype=None):
+    """numpy -> device tensor.  Arrays of at least ``host_streaming_min_bytes``
+    are page-locked in place and copied by DMA (no pageable staging copy);
+    smaller ones take torch's copy."""
+    if not isinstance(arr, np.ndarray):
+        return to_device(arr, device, dtype)
+    arr = np.ascontiguousarray(arr if dtype is None else arr.astype(dtype, copy=False))
+    if arr.nbytes < max(1, get_options()["host_streaming_min_bytes"]) or \
+            arr.dtype not in _native.DTYPE_CODES:
+        return to_device(arr, device)
+    dst = empty(arr.shape, arr.dtype, device)
+    stream = torch().cuda.current_stream(device)
+    with HostPin(arr):
+        try:
+            _copy(dst.data_ptr(), arr.ctypes.data, arr.nbytes, stream)
+        finally:   # the copy has landed before the array is unpinned
+            stream.synchronize()
+    return dst
+
+
+def device_to_host(x) -> np.ndarray:
+    """device tensor -> numpy, by DMA into a page-locked result for tensors of
+    at least ``host_streaming_min_bytes``."""
+    nbytes = x.numel() * x.element_size()
+    if nbytes < max(1, get_options()["host_streaming_min_bytes"]):
+        return x.cpu().numpy()
+    x = x.contiguous()
+    out = np.empty(tuple(x.shape), numpy_dtype(x.dtype))
+    stream = torch().cuda.current_stream(x.device)
+    with HostPin(out):
+        try:
+            _copy(out.ctypes.data, x.data_ptr(), nbytes, stream)
+        finally:
+            stream.synchronize()
+    return out
 
 
 def band_ranges(height: int, band_rows: int) -> list[tuple[int, int]]:
