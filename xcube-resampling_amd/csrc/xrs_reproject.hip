@@ -355,11 +355,20 @@ gather_separable_mlp_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t ba
             const int32_t f = max(cf[k], 0), c = max(cc[k], 0);
             v[q][0][k] = rf[f];
             if (INTERP != XRS_INTERP_NEAREST) {
-              v[q][1][k] = rf[c];
+              if (DBG != 2) v[q][1][k] = rf[c];
               v[q][2][k] = rc[f];
-              v[q][3][k] = rc[c];
+              if (DBG != 2) v[q][3][k] = rc[c];
             }
           }
+        }
+        if (DBG == 2) {   // timing probe: ceil taps from the next lane (wrong values)
+#pragma unroll
+          for (int q = 0; q < kRowsB; ++q)
+#pragma unroll
+            for (int k = 0; k < PX; ++k) {
+              v[q][1][k] = __shfl_down(v[q][0][k], 1);
+              v[q][3][k] = __shfl_down(v[q][2][k], 1);
+            }
         }
 #pragma unroll
         for (int q = 0; q < kRowsB; ++q) {
@@ -1191,6 +1200,12 @@ gather_wave_staged_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t band
 //   24     variant-12 gathers (4 rows x 4 columns per lane) with the output
 //          row transposed through LDS into 16-byte stores: 2.88 vs 2.66 ms
 //          (8192^2: 0.125 vs 0.110) — the dword stores are not the limit either
+//   90/91  timing probes (wrong values): 90 drops the float64 lerps (2.49 vs
+//          2.65 ms), 91 takes the two ceil-column taps from the next lane by
+//          shuffle instead of loading them (2.67 ms: no gain).  Nearest in the
+//          same run: 2.33 ms.  So bilinear costs the nearest gather (~copy rate)
+//          plus ~0.16 ms of float64 lerp (required for bit-exact parity) plus
+//          ~0.16 ms for the second source row — not tap-issue bound.
 inline int variant() {
   const char* v = getenv("XRS_REPROJECT_VARIANT");
   return v ? atoi(v) : 12;
@@ -1207,7 +1222,7 @@ int launch(const GatherArgs& a, int coord_mode, AxisEntry* xtab, AxisEntry* ytab
   if (variant() == 14 && args.g.band > 64) args.g.band = 64;   // rows_s capacity
   const int64_t bands_per_tile = (g.tile_h + args.g.band - 1) / args.g.band;
   const int v = variant();
-  args.g.segw = kThreads * (v == 9 || v == 12 || v == 13 || v == 14 || v == 90 || v == 21 || v == 22 ? 2 : v == 10 ? 8 : (v == 20 || v == 23 || v == 24) ? 4 : v == 11 ? 1 : kPx);
+  args.g.segw = kThreads * (v == 9 || v == 12 || v == 13 || v == 14 || v == 90 || v == 91 || v == 21 || v == 22 ? 2 : v == 10 ? 8 : (v == 20 || v == 23 || v == 24) ? 4 : v == 11 ? 1 : kPx);
   const int64_t segs_per_tile = (g.tile_w + args.g.segw - 1) / args.g.segw;
   const int64_t nsegs = g.ntiles_x * segs_per_tile;
   const int64_t nwork = (ty1 - ty0) * bands_per_tile * nsegs;
@@ -1286,7 +1301,11 @@ int launch(const GatherArgs& a, int coord_mode, AxisEntry* xtab, AxisEntry* ytab
         hipLaunchKernelGGL((gather_wave_staged_kernel<T, O, INTERP, false>), dim3(nb),
                            dim3(kThreads), lds, stream, args, ty0, nsegs, bands_per_tile,
                            segs_per_tile, nwork);
-    } else if (v == 90)   // timing probe only: bilinear loads, f32 sum instead of the f64 lerps
+    } else if (v == 91)   // timing probe only: 2 of the 4 taps by cross-lane shuffle
+      hipLaunchKernelGGL((gather_separable_mlp_kernel<T, O, INTERP, 8, true, 2, 2>), dim3(nb),
+                         dim3(kThreads), 0, stream, args, ty0, nsegs, bands_per_tile,
+                         segs_per_tile, nwork);
+    else if (v == 90)   // timing probe only: bilinear loads, f32 sum instead of the f64 lerps
       hipLaunchKernelGGL((gather_separable_mlp_kernel<T, O, INTERP, 8, true, 2, 1>), dim3(nb),
                          dim3(kThreads), 0, stream, args, ty0, nsegs, bands_per_tile,
                          segs_per_tile, nwork);
