@@ -657,50 +657,6 @@ __device__ inline void load_run(const T* p, T (&v)[DX]) {
   for (int c = 0; c < DX; ++c) v[c] = p[c];
 }
 
-// Exact path of one K3i pixel: every sub-sample through Taps (scipy's sum).
-template <typename T, int ORDER, int D>
-__device__ inline void integral_exact_pixel(
-    const T* g0, const T* g1, int64_t sy, bool two, const AxisTab* yrow, const AxisTab* xrun,
-    int agg, double cval, void* dst, int dst_dtype, int64_t didx) {
-  Src<T> p;
-  p.g0 = g0;
-  p.g1 = g1;
-  p.sy = sy;
-  AffineArgs a;   // only what Fold::store reads
-  a.agg = agg;
-  a.dst = dst;
-  a.dst_dtype = dst_dtype;
-  // table entries first, then one sub-sample row's taps at a time, all in
-  // flight together (D + 1 memory round trips instead of 2*D*D)
-  AxisTab ey[D], ex[D];
-#pragma unroll
-  for (int k = 0; k < D; ++k) {
-    ey[k] = yrow[k];
-    ex[k] = xrun[k];
-  }
-  Fold<T> fold;
-#pragma unroll
-  for (int sj = 0; sj < D; ++sj) {
-    Taps<T> tp[D];
-    T sv[D];
-    if (ORDER == 1 && two) {
-#pragma unroll
-      for (int si = 0; si < D; ++si) tp[si].template load<ORDER, true>(p, ey[sj], ex[si]);
-#pragma unroll
-      for (int si = 0; si < D; ++si)
-        sv[si] = tp[si].template eval<T, ORDER, false, true>(ey[sj], ex[si], cval);
-    } else {
-#pragma unroll
-      for (int si = 0; si < D; ++si) tp[si].template load<ORDER, false>(p, ey[sj], ex[si]);
-#pragma unroll
-      for (int si = 0; si < D; ++si)
-        sv[si] = tp[si].template eval<T, ORDER, false, false>(ey[sj], ex[si], cval);
-    }
-    fold.add_row(agg, D, [&](int si) -> T { return sv[si]; });
-  }
-  fold.store(a, didx);
-}
-
 template <typename T, int ORDER, int D, bool TWO>
 __global__ void __launch_bounds__(kThreads)
 affine_reduce_integral_kernel(AffineArgs a, const AxisTab* __restrict__ ytab,
@@ -838,27 +794,61 @@ affine_reduce_integral_kernel(AffineArgs a, const AxisTab* __restrict__ ytab,
   }
 }
 
-// K3i's slow pixels (exact path), one thread per listed pixel.  Runs only
-// when K3i worked and its list fit (else the generic K3 redid the launch).
+// K3i's slow pixels (exact path).  Lanes work on sub-samples, not pixels: a
+// wave takes 64 / D^2 listed pixels, lane l evaluates sub-sample l % D^2 of
+// its pixel through Taps (scipy's sum; all loads of a wave in flight
+// together), and the pixel's first lane folds the D^2 values in numpy's order.
+// Runs only when K3i worked and its list fit (else the generic K3 redid the
+// launch).
 template <typename T, int ORDER, int D>
 __global__ void __launch_bounds__(kThreads)
 integral_slow_kernel(AffineArgs a, const AxisTab* __restrict__ ytab,
                      const AxisTab* __restrict__ xtab, const int32_t* __restrict__ nonint,
                      int32_t nonint_limit, const int64_t* __restrict__ slow_list,
                      int64_t slow_cap) {
+  constexpr int S = D * D;     // sub-samples per pixel
+  constexpr int G = 64 / S;    // pixels per wave
   const int64_t n = nonint[2];
   if (nonint[0] > nonint_limit || n > slow_cap) return;
-  for (int64_t k = (int64_t)blockIdx.x * kThreads + threadIdx.x; k < n;
-       k += (int64_t)gridDim.x * kThreads) {
-    const int64_t idx = slow_list[k];
-    const int64_t oi = idx % a.out_w, rest = idx / a.out_w;
-    const int64_t oj = rest % a.out_h, t = rest / a.out_h;
-    const T* g0 = static_cast<const T*>(a.src) + t * a.src_st;
-    const int64_t t1 = (ORDER == 1 && a.t_next) ? a.t_next[t] : -1;
-    const T* g1 = t1 >= 0 ? static_cast<const T*>(a.src) + t1 * a.src_st : g0;
-    integral_exact_pixel<T, ORDER, D>(g0, g1, a.src_sy, t1 >= 0, ytab + oj * D, xtab + oi * D,
-                                      a.agg, a.cval, a.dst, a.dst_dtype,
-                                      t * a.dst_st + oj * a.dst_sy + oi);
+  const int lane = threadIdx.x & 63;
+  const int grp = lane / S, sub = lane % S, sj = sub / D, si = sub % D;
+  const int64_t nw = (int64_t)gridDim.x * (kThreads / 64);
+  // wave-uniform trip count: the shuffles below always see all 64 lanes
+  for (int64_t w = (int64_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6); w * G < n;
+       w += nw) {
+    const int64_t k = w * G + grp;
+    const bool valid = grp < G && k < n;
+    T val = (T)0;
+    int64_t didx = 0;
+    if (valid) {
+      const int64_t idx = slow_list[k];
+      const int64_t oi = idx % a.out_w, rest = idx / a.out_w;
+      const int64_t oj = rest % a.out_h, t = rest / a.out_h;
+      const int64_t t1 = (ORDER == 1 && a.t_next) ? a.t_next[t] : -1;
+      Src<T> p;
+      p.g0 = static_cast<const T*>(a.src) + t * a.src_st;
+      p.g1 = t1 >= 0 ? static_cast<const T*>(a.src) + t1 * a.src_st : p.g0;
+      p.sy = a.src_sy;
+      const AxisTab ey = ytab[oj * D + sj], ex = xtab[oi * D + si];
+      Taps<T> tp;
+      if (ORDER == 1 && t1 >= 0) {
+        tp.template load<ORDER, true>(p, ey, ex);
+        val = tp.template eval<T, ORDER, false, true>(ey, ex, a.cval);
+      } else {
+        tp.template load<ORDER, false>(p, ey, ex);
+        val = tp.template eval<T, ORDER, false, false>(ey, ex, a.cval);
+      }
+      didx = t * a.dst_st + oj * a.dst_sy + oi;
+    }
+    T vals[S];
+#pragma unroll
+    for (int i = 0; i < S; ++i) vals[i] = __shfl(val, (grp < G ? grp : 0) * S + i, 64);
+    if (valid && sub == 0) {
+      Fold<T> fold;
+#pragma unroll
+      for (int r = 0; r < D; ++r) fold.add_row(a.agg, D, [&](int c) { return vals[r * D + c]; });
+      fold.store(a, didx);
+    }
   }
 }
 
@@ -1003,7 +993,7 @@ int launch(const AffineArgs& a, const AxisChunks& ay, const AxisChunks& ax, Axis
   if (k3i) {
     if constexpr (std::is_floating_point<T>::value && std::is_same<T, I>::value && !RECOVER) {
 #define XRS_K3S(D)                                                                        \
-  hipLaunchKernelGGL((integral_slow_kernel<T, ORDER, D>), dim3(256), dim3(kThreads), 0, st, \
+  hipLaunchKernelGGL((integral_slow_kernel<T, ORDER, D>), dim3(1024), dim3(kThreads), 0, st, \
                      args, ytab, xtab, nonint, limit, slow_list, slow_cap)
       if (a.dx == 2) XRS_K3S(2);
       else if (a.dx == 4) XRS_K3S(4);
