@@ -746,8 +746,54 @@ affine_reduce_integral_kernel(AffineArgs a, const AxisTab* __restrict__ ytab,
       if (q >= nrows) break;
       const int64_t oj = oj0 + q;
       const int64_t didx = t * a.dst_st + oj * a.dst_sy + oi;
+      if (!active) continue;
+      const bool lean = a.agg == AGG_MEAN || a.agg == AGG_SUM;
       bool slow = !fast;
-      if (ORDER == 1 && fast) {   // zero-weight taps: right column, row below, t+1
+      if (fast && lean) {
+        // The values' sum equals numpy's whatever their zero signs (a signed
+        // zero only flips the sign of a zero partial, and the total starts at
+        // +0), so the -0 -> +0 map is not needed here.  Order 1: every value
+        // and zero-weight tap is finite iff their sums are (an overflow to
+        // inf only sends the pixel to the exact path).
+        T total = (T)0;
+        int cnt = D * D;
+        if (ORDER == 1) {
+#pragma unroll
+          for (int sj = 0; sj < D; ++sj)
+            total = total + pairwise_row<T>(D, [&](int si) { return v[q * D + sj][si]; });
+          T extra = (T)0;   // zero-weight taps: right column, row below, t+1
+#pragma unroll
+          for (int r = q * D; r <= q * D + D; ++r) {
+            extra = extra + nbv[r];
+            if (T1) extra = extra + nbv1[T1 ? r : 0];
+          }
+#pragma unroll
+          for (int c = 0; c < D; ++c) extra = extra + v[q * D + D][c];
+          if (T1) {
+#pragma unroll
+            for (int r = q * D; r <= q * D + D; ++r)
+#pragma unroll
+              for (int c = 0; c < D; ++c) extra = extra + v1[T1 ? r : 0][c];
+          }
+          slow = !is_finite(total) || !is_finite(extra);
+        } else {   // order 0: NaN values are skipped by the nan-reducers
+          cnt = 0;
+#pragma unroll
+          for (int sj = 0; sj < D; ++sj)
+            total = total + pairwise_row<T>(D, [&](int si) {
+              const T x = v[q * D + sj][si];
+              const bool nan = x != x;
+              cnt += nan ? 0 : 1;
+              return nan ? (T)0 : x;
+            });
+        }
+        if (!slow) {
+          const double res = a.agg == AGG_MEAN ? (double)(T)((double)total / (double)cnt)
+                                               : (double)total;
+          store_any(a.dst, didx, a.dst_dtype, res, 0, false);
+          continue;
+        }
+      } else if (ORDER == 1 && fast) {   // zero-weight taps: right column, row below, t+1
 #pragma unroll
         for (int r = q * D; r <= q * D + D; ++r) {
           slow = slow || !is_finite(nbv[r]);
@@ -759,37 +805,20 @@ affine_reduce_integral_kernel(AffineArgs a, const AxisTab* __restrict__ ytab,
           }
         }
       }
-      if (!active) continue;
       if (slow) {   // the exact path runs in integral_slow_kernel (keeps its
                     // registers out of this streaming kernel)
         const int32_t k = atomicAdd(nslow, 1);
         if (k < slow_cap) slow_list[k] = (t * a.out_h + oj) * a.out_w + oi;
         continue;
       }
-      auto sub = [&](int sj, int si) -> T {
-        const T x = v[q * D + sj][si];
-        return x == (T)0 ? (T)0 : x;   // scipy's 0.0 + w*x: -0 -> +0
-      };
-      if (a.agg == AGG_MEAN || a.agg == AGG_SUM) {   // the common case, lean
-        T total = (T)0;
-        int cnt = 0;
+      Fold<T> fold;
 #pragma unroll
-        for (int sj = 0; sj < D; ++sj)
-          total = total + pairwise_row<T>(D, [&](int si) {
-            const T x = sub(sj, si);
-            const bool nan = x != x;
-            cnt += nan ? 0 : 1;
-            return nan ? (T)0 : x;
-          });
-        const double res = a.agg == AGG_MEAN ? (double)(T)((double)total / (double)cnt)
-                                             : (double)total;
-        store_any(a.dst, didx, a.dst_dtype, res, 0, false);
-      } else {
-        Fold<T> fold;
-#pragma unroll
-        for (int sj = 0; sj < D; ++sj) fold.add_row(a.agg, D, [&](int si) { return sub(sj, si); });
-        fold.store(a, didx);
-      }
+      for (int sj = 0; sj < D; ++sj)
+        fold.add_row(a.agg, D, [&](int si) {
+          const T x = v[q * D + sj][si];
+          return x == (T)0 ? (T)0 : x;   // scipy's 0.0 + w*x: -0 -> +0
+        });
+      fold.store(a, didx);
     }
   }
 }
