@@ -175,13 +175,26 @@ ij_bboxes_kernel(BBoxArgs a, int64_t chunk) {
     }
     int32_t cur = valid ? next_box(a, bx, x, y, tx0, tx1, ty0, ty1, -1) : INT32_MAX;
     while (true) {
-      const int32_t k = wave_min(cur);  // next box any lane of the wave contributes to
+      // next box any lane of the wave contributes to; usually every lane's
+      const int32_t c0 = __builtin_amdgcn_readfirstlane(cur);
+      const bool uni = __all(cur == c0);
+      const int32_t k = uni ? c0 : wave_min(cur);
       if (k == INT32_MAX) break;
       const bool mine = cur == k;
-      const int32_t imin = wave_min(mine ? i0 : INT32_MAX);
-      const int32_t jmin = wave_min(mine ? j0 : INT32_MAX);
-      const int32_t imax = wave_max(mine ? i0 : -1);
-      const int32_t jmax = wave_max(mine ? j0 : -1);
+      int32_t imin, jmin, imax, jmax;
+      const int32_t jf = __builtin_amdgcn_readfirstlane(j0);
+      if (uni && __builtin_amdgcn_readlane(j0, 63) == jf) {
+        // every lane, one source row: lanes hold consecutive pixels, so the
+        // extremes are the first and the last lane's
+        imin = __builtin_amdgcn_readfirstlane(i0);
+        imax = __builtin_amdgcn_readlane(i0, 63);
+        jmin = jmax = jf;
+      } else {
+        imin = wave_min(mine ? i0 : INT32_MAX);
+        jmin = wave_min(mine ? j0 : INT32_MAX);
+        imax = wave_max(mine ? i0 : -1);
+        jmax = wave_max(mine ? j0 : -1);
+      }
       if ((threadIdx.x & 63) == 0) {
         atomicMin(&acc[4 * k + 0], imin);
         atomicMin(&acc[4 * k + 1], jmin);
