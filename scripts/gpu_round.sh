@@ -12,7 +12,7 @@ if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "pytest ended with status $rc"; exi
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
 timeout -k 10 300 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err
 cat $OUT/bench.json
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o bench -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline > $OUT/bench_prof.json 2> $OUT/bench_prof.err
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o bench -- python3 bench.py --no-cpu-baseline > $OUT/bench_prof.json 2> $OUT/bench_prof.err
 timeout -k 10 400 python -u scripts/bench_configs.py > $OUT/configs.jsonl 2> $OUT/configs.err
 cat $OUT/configs.jsonl
 exit $rc
