@@ -24,13 +24,16 @@ import ctypes
 import numpy as np
 
 from . import _native, kernels
+from .constants import LOG
 from .device import empty, numpy_dtype, require_device, stream_handle, to_device, torch
 from .options import get_options
 
 
 class HostPin:
     """Page-lock a C-contiguous numpy array in place for the lifetime of the
-    context (no copy).  Memory that is already registered stays as it is."""
+    context (no copy).  Memory that is already registered stays as it is;
+    memory the runtime refuses to lock (e.g. a file-backed np.memmap) stays
+    pageable — the copies are then staged by the runtime: slower, same bytes."""
 
     def __init__(self, array: np.ndarray):
         if not array.flags.c_contiguous:
@@ -42,8 +45,11 @@ class HostPin:
         if self.array.nbytes:
             rc = _native.lib().xrs_host_register(
                 ctypes.c_void_p(self.array.ctypes.data), self.array.nbytes)
-            if rc < 0:
+            if rc == _native.XRS_ERR_ARG:
                 _native.check(rc, "xrs_host_register")
+            if rc == _native.XRS_ERR_HIP:
+                LOG.debug("host array not page-locked (%s); copies are staged",
+                          _native.last_error())
             self._registered = rc == _native.XRS_OK
         return self.array
 
