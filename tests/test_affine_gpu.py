@@ -284,3 +284,36 @@ def test_integral_coarsen_slow_list(nan_frac, order):
                                     np.nan)
             got = got if isinstance(got, np.ndarray) else got.cpu().numpy()
             assert_bitwise_equal(got, np.asarray(ref), f"{dtype} d={d} {agg} nan={nan_frac}")
+
+
+def test_config3_full_size_sampled_blocks():
+    """BASELINE config 3 at full size — coarsen mean 4x4 of a 16384^2 float32
+    raster (K3i, one launch): 1024^2-source blocks at the corners and the centre
+    == the oracle (dask-image chunk footprint + scipy order 1 + numpy nanmean
+    in dask chunk.coarsen order) on the same block, bit for bit (the block's
+    own last output row/column excluded: there the standalone block mirrors its
+    edge, the full raster does not)."""
+    import torch
+
+    import xcube_resampling_amd.affine as A
+    from oracle import affine_ref
+    from xcube_resampling_amd import kernels
+
+    n, k = 16384, 4
+    m = ((4.0, 0.0, 0.0), (0.0, 4.0, 0.0))
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(9)
+    src = torch.rand((1, n, n), generator=gen, device="cuda", dtype=torch.float32)
+    plan = A.plan_affine(tuple(src.shape), np.dtype(np.float32), m, (1, n // k, n // k),
+                         (1, 512, 512), 1, "mean", False, np.nan)
+    out = kernels.affine(src, plan)
+    c = 1024
+    for r0, c0 in [(0, 0), (0, n - c), (n // 2, n // 2), (n - c, 0), (n - c, n - c)]:
+        a = src[:, r0:r0 + c, c0:c0 + c].cpu().numpy()
+        ref = affine_ref.resample_array(a, m, (1, c // k, c // k), (1, c // k, c // k), 1,
+                                        "mean", False, np.nan)
+        got = out[:, r0 // k:(r0 + c) // k, c0 // k:(c0 + c) // k].cpu().numpy()
+        last = r0 + c == n, c0 + c == n   # the raster's own edge: mirrored in both
+        assert_bitwise_equal(got[:, :None if last[0] else -1, :None if last[1] else -1],
+                             ref[:, :None if last[0] else -1, :None if last[1] else -1],
+                             f"block at ({r0}, {c0})")
