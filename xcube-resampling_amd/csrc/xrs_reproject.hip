@@ -356,8 +356,28 @@ gather_separable_mlp_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t ba
             v[q][0][k] = rf[f];
             if (INTERP != XRS_INTERP_NEAREST) {
               if (DBG != 2) v[q][1][k] = rf[c];
-              v[q][2][k] = rc[f];
-              if (DBG != 2) v[q][3][k] = rc[c];
+              if (DBG != 3 && DBG != 4) v[q][2][k] = rc[f];
+              if (DBG != 2 && DBG != 3 && DBG != 4) v[q][3][k] = rc[c];
+              if (DBG == 3) { v[q][2][k] = v[q][0][k]; v[q][3][k] = v[q][1][k]; }
+            }
+          }
+        }
+        if (DBG == 4 && INTERP != XRS_INTERP_NEAREST) {
+          // two phases: the ceil rows are requested only once the floor rows
+          // have landed, so a ceil row that is the next target row's floor row
+          // hits L1 instead of sending a second request to L2 for the same
+          // lines (in flight together, the two requests do not merge).  The
+          // opaque zero makes the ceil addresses depend on the last floor load.
+          int32_t z;
+          asm volatile("v_and_b32 %0, 0, %1" : "=v"(z)
+                       : "v"(__float_as_int((float)v[kRowsB - 1][1][PX - 1])));
+#pragma unroll
+          for (int q = 0; q < kRowsB; ++q) {
+            const T* rc = src + (int64_t)max(ye[q].c, 0) * a.src_sy + z;
+#pragma unroll
+            for (int k = 0; k < PX; ++k) {
+              v[q][2][k] = rc[max(cf[k], 0)];
+              v[q][3][k] = rc[max(cc[k], 0)];
             }
           }
         }
@@ -1206,6 +1226,13 @@ gather_wave_staged_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t band
 //          same run: 2.33 ms.  So bilinear costs the nearest gather (~copy rate)
 //          plus ~0.16 ms of float64 lerp (required for bit-exact parity) plus
 //          ~0.16 ms for the second source row — not tap-issue bound.
+//   92     probe: the ceil row's taps not loaded (floor row reused): 2.21-2.37
+//          vs 2.45-2.65 ms — the second row fetch (the same lines requested
+//          again while the first request is in flight) is the cost.  Fixes
+//          tried, all bit-identical and slower: 25 (ceil rows requested after
+//          the floor rows landed, so they hit L1): 4.20 ms; each source row of
+//          a batch loaded once into register vectors and picked by a
+//          wave-uniform index (GPR indexing mode, 10/13-row windows): 5.1 ms.
 inline int variant() {
   const char* v = getenv("XRS_REPROJECT_VARIANT");
   return v ? atoi(v) : 12;
@@ -1222,7 +1249,7 @@ int launch(const GatherArgs& a, int coord_mode, AxisEntry* xtab, AxisEntry* ytab
   if (variant() == 14 && args.g.band > 64) args.g.band = 64;   // rows_s capacity
   const int64_t bands_per_tile = (g.tile_h + args.g.band - 1) / args.g.band;
   const int v = variant();
-  args.g.segw = kThreads * (v == 9 || v == 12 || v == 13 || v == 14 || v == 90 || v == 91 || v == 21 || v == 22 ? 2 : v == 10 ? 8 : (v == 20 || v == 23 || v == 24) ? 4 : v == 11 ? 1 : kPx);
+  args.g.segw = kThreads * (v == 9 || v == 12 || v == 13 || v == 14 || v == 90 || v == 91 || v == 92 || v == 25 || v == 21 || v == 22 ? 2 : v == 10 ? 8 : (v == 20 || v == 23 || v == 24) ? 4 : v == 11 ? 1 : kPx);
   const int64_t segs_per_tile = (g.tile_w + args.g.segw - 1) / args.g.segw;
   const int64_t nsegs = g.ntiles_x * segs_per_tile;
   const int64_t nwork = (ty1 - ty0) * bands_per_tile * nsegs;
@@ -1301,7 +1328,15 @@ int launch(const GatherArgs& a, int coord_mode, AxisEntry* xtab, AxisEntry* ytab
         hipLaunchKernelGGL((gather_wave_staged_kernel<T, O, INTERP, false>), dim3(nb),
                            dim3(kThreads), lds, stream, args, ty0, nsegs, bands_per_tile,
                            segs_per_tile, nwork);
-    } else if (v == 91)   // timing probe only: 2 of the 4 taps by cross-lane shuffle
+    } else if (v == 25)   // two-phase row loads (floor rows, then ceil rows)
+      hipLaunchKernelGGL((gather_separable_mlp_kernel<T, O, INTERP, 8, true, 2, 4>), dim3(nb),
+                         dim3(kThreads), 0, stream, args, ty0, nsegs, bands_per_tile,
+                         segs_per_tile, nwork);
+    else if (v == 92)   // timing probe only: the ceil row's taps not loaded (floor row reused)
+      hipLaunchKernelGGL((gather_separable_mlp_kernel<T, O, INTERP, 8, true, 2, 3>), dim3(nb),
+                         dim3(kThreads), 0, stream, args, ty0, nsegs, bands_per_tile,
+                         segs_per_tile, nwork);
+    else if (v == 91)   // timing probe only: 2 of the 4 taps by cross-lane shuffle
       hipLaunchKernelGGL((gather_separable_mlp_kernel<T, O, INTERP, 8, true, 2, 2>), dim3(nb),
                          dim3(kThreads), 0, stream, args, ty0, nsegs, bands_per_tile,
                          segs_per_tile, nwork);
