@@ -356,9 +356,28 @@ gather_separable_mlp_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t ba
             v[q][0][k] = rf[f];
             if (INTERP != XRS_INTERP_NEAREST) {
               if (DBG != 2) v[q][1][k] = rf[c];
-              if (DBG != 3 && DBG != 4) v[q][2][k] = rc[f];
-              if (DBG != 2 && DBG != 3 && DBG != 4) v[q][3][k] = rc[c];
+              if (DBG != 3 && DBG != 4 && DBG != 5) v[q][2][k] = rc[f];
+              if (DBG != 2 && DBG != 3 && DBG != 4 && DBG != 5) v[q][3][k] = rc[c];
               if (DBG == 3) { v[q][2][k] = v[q][0][k]; v[q][3][k] = v[q][1][k]; }
+            }
+          }
+        }
+        // DBG 5: a ceil row that is the next target row's floor row is not
+        // fetched again: the taps come from that row's registers (uniform
+        // test; the loads of the other ceil rows sit in uniform branches)
+        bool share[kRowsB];
+#pragma unroll
+        for (int q = 0; q < kRowsB; ++q)
+          share[q] = DBG == 5 && q + 1 < kRowsB && ye[q].c == ye[q + 1].f;
+        if (DBG == 5 && INTERP != XRS_INTERP_NEAREST) {
+#pragma unroll
+          for (int q = 0; q < kRowsB; ++q) {
+            if (share[q]) continue;
+            const T* rc = src + (int64_t)max(ye[q].c, 0) * a.src_sy;
+#pragma unroll
+            for (int k = 0; k < PX; ++k) {
+              v[q][2][k] = rc[max(cf[k], 0)];
+              v[q][3][k] = rc[max(cc[k], 0)];
             }
           }
         }
@@ -404,8 +423,10 @@ gather_separable_mlp_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t ba
               out = (O)v00;
             } else {
               const T v01 = (okf && xc) ? v[q][1][k] : fill;
-              const T v10 = (okc && xf) ? v[q][2][k] : fill;
-              const T v11 = (okc && xc) ? v[q][3][k] : fill;
+              const T c0 = share[q] ? v[q + 1 < kRowsB ? q + 1 : q][0][k] : v[q][2][k];
+              const T c1 = share[q] ? v[q + 1 < kRowsB ? q + 1 : q][1][k] : v[q][3][k];
+              const T v10 = (okc && xf) ? c0 : fill;
+              const T v11 = (okc && xc) ? c1 : fill;
               if (DBG == 1) out = (O)(v00 + v01 + v10 + v11);
               else out = Conv<O>::from_f64(interp4<T, INTERP>(v00, v01, v10, v11, dx[k], ye[q].d));
             }
@@ -1232,7 +1253,11 @@ gather_wave_staged_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t band
 //          tried, all bit-identical and slower: 25 (ceil rows requested after
 //          the floor rows landed, so they hit L1): 4.20 ms; each source row of
 //          a batch loaded once into register vectors and picked by a
-//          wave-uniform index (GPR indexing mode, 10/13-row windows): 5.1 ms.
+//          wave-uniform index (GPR indexing mode, 10/13-row windows): 5.1 ms;
+//          28 (a ceil row equal to the next target row's floor row taken from
+//          that row's registers, the other ceil rows loaded in uniform
+//          branches): 2.63 vs 2.51 ms — the branches and the partial waits they
+//          bring cost more than the saved fetches.
 inline int variant() {
   const char* v = getenv("XRS_REPROJECT_VARIANT");
   return v ? atoi(v) : 12;
@@ -1249,7 +1274,7 @@ int launch(const GatherArgs& a, int coord_mode, AxisEntry* xtab, AxisEntry* ytab
   if (variant() == 14 && args.g.band > 64) args.g.band = 64;   // rows_s capacity
   const int64_t bands_per_tile = (g.tile_h + args.g.band - 1) / args.g.band;
   const int v = variant();
-  args.g.segw = kThreads * (v == 9 || v == 12 || v == 13 || v == 14 || v == 90 || v == 91 || v == 92 || v == 25 || v == 21 || v == 22 ? 2 : v == 10 ? 8 : (v == 20 || v == 23 || v == 24) ? 4 : v == 11 ? 1 : kPx);
+  args.g.segw = kThreads * (v == 9 || v == 12 || v == 13 || v == 14 || v == 90 || v == 91 || v == 92 || v == 25 || v == 28 || v == 21 || v == 22 ? 2 : v == 10 ? 8 : (v == 20 || v == 23 || v == 24) ? 4 : v == 11 ? 1 : kPx);
   const int64_t segs_per_tile = (g.tile_w + args.g.segw - 1) / args.g.segw;
   const int64_t nsegs = g.ntiles_x * segs_per_tile;
   const int64_t nwork = (ty1 - ty0) * bands_per_tile * nsegs;
@@ -1328,7 +1353,11 @@ int launch(const GatherArgs& a, int coord_mode, AxisEntry* xtab, AxisEntry* ytab
         hipLaunchKernelGGL((gather_wave_staged_kernel<T, O, INTERP, false>), dim3(nb),
                            dim3(kThreads), lds, stream, args, ty0, nsegs, bands_per_tile,
                            segs_per_tile, nwork);
-    } else if (v == 25)   // two-phase row loads (floor rows, then ceil rows)
+    } else if (v == 28)   // ceil rows shared with the next target row's floor row
+      hipLaunchKernelGGL((gather_separable_mlp_kernel<T, O, INTERP, 8, true, 2, 5>), dim3(nb),
+                         dim3(kThreads), 0, stream, args, ty0, nsegs, bands_per_tile,
+                         segs_per_tile, nwork);
+    else if (v == 25)   // two-phase row loads (floor rows, then ceil rows)
       hipLaunchKernelGGL((gather_separable_mlp_kernel<T, O, INTERP, 8, true, 2, 4>), dim3(nb),
                          dim3(kThreads), 0, stream, args, ty0, nsegs, bands_per_tile,
                          segs_per_tile, nwork);
