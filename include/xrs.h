@@ -286,6 +286,26 @@ int xrs_rectify_var(const double* ij, int64_t dst_h, int64_t dst_w, const void* 
                     int64_t src_sy, void* dst, int64_t dst_sn, int interp, double fill,
                     void* stream);
 
+/* -------------------------------------------------------------------------
+ * Test-only path selection.  Every kernel has ONE schedule per case; these
+ * knobs only force alternative, bit-identical code paths (or work shapes) so
+ * that the parity tests can cover them.  Nothing reads the environment: a
+ * process that never calls xrs_testing_set() runs the product paths.
+ *   XRS_TESTING_REPROJECT_BAND            target rows per K1 work item (0 = 32)
+ *   XRS_TESTING_REPROJECT_BLOCKS_PER_CU   cap K1's grid (grid-stride loop; 0 = none)
+ *   XRS_TESTING_AFFINE_GENERIC            1: aligned integer coarsens take the
+ *                                         generic K3 instead of K3i
+ *   XRS_TESTING_RECTIFY_EXACT             1: K5 decides every triangle test and
+ *                                         pixel floor by the exact division
+ * Returns the previous value (or XRS_ERR_ARG for an unknown knob).
+ * ------------------------------------------------------------------------- */
+#define XRS_TESTING_REPROJECT_BAND 1
+#define XRS_TESTING_REPROJECT_BLOCKS_PER_CU 2
+#define XRS_TESTING_AFFINE_GENERIC 3
+#define XRS_TESTING_RECTIFY_EXACT 4
+#define XRS_TESTING_NUM_KNOBS 8
+int64_t xrs_testing_set(int knob, int64_t value);
+
 #ifdef __cplusplus
 }
 #endif

@@ -104,3 +104,44 @@ def transform_bounds(transform, left, bottom, right, top, densify_pts=21):
     tx, ty = transform(xs, ys)
     ok = np.isfinite(tx) & np.isfinite(ty)
     return float(tx[ok].min()), float(ty[ok].min()), float(tx[ok].max()), float(ty[ok].max())
+
+
+# --------------------------------------------------------------------------
+# affine-package matrix arithmetic (affine >= 2.2, not installed here; its
+# published __invert__ / __mul__ restated) as used by
+# gridmapping/base.py:437-478 (ij_to_xy_transform, xy_to_ij_transform,
+# ij_transform_to) through helpers.py:51-56 (_from_affine / _to_affine)
+# --------------------------------------------------------------------------
+
+def affine_invert(m):
+    """affine.Affine.__invert__: idet = 1 / (a*e - b*d), then the closed form."""
+    (a, b, c), (d, e, f) = m
+    idet = 1.0 / (a * e - b * d)
+    ra = e * idet
+    rb = -b * idet
+    rd = -d * idet
+    re = a * idet
+    return (ra, rb, -c * ra - f * rb), (rd, re, -c * rd - f * re)
+
+
+def affine_mul(s, o):
+    """affine.Affine.__mul__ (s * o, both 2x3)."""
+    (sa, sb, sc), (sd, se, sf) = s
+    (oa, ob, oc), (od, oe, of) = o
+    return ((sa * oa + sb * od, sa * ob + sb * oe, sa * oc + sb * of + sc),
+            (sd * oa + se * od, sd * ob + se * oe, sd * oc + se * of + sf))
+
+
+def ij_to_xy_transform(xy_bbox, xy_res, is_j_axis_up=False):
+    """base.py:437-451."""
+    x_min, y_min, _, y_max = xy_bbox
+    x_res, y_res = xy_res
+    if is_j_axis_up:
+        return (x_res, 0.0, x_min), (0.0, y_res, y_min)
+    return (x_res, 0.0, x_min), (0.0, -y_res, y_max)
+
+
+def ij_transform_to(src_ij_to_xy, tgt_ij_to_xy):
+    """base.py:461-478 with self = target, other = source: image coordinates
+    of the target -> image coordinates of the source (affine.py:121)."""
+    return affine_mul(affine_invert(src_ij_to_xy), tgt_ij_to_xy)

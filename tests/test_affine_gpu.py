@@ -181,41 +181,13 @@ def test_integral_grid_coarsen_special_values(dtype, nd, agg, order):
         assert_bitwise_equal(got, np.asarray(ref), f"{dtype} {agg} order={order} {m}")
 
 
-@pytest.mark.parametrize("stage", ["0", "1"])
-def test_reduce_lds_stage_knob_bit_identical(stage, monkeypatch):
-    """K3 with the tile source footprint staged in LDS (XRS_AFFINE_STAGE=1) and
-    with direct global taps give the same bits as the oracle (random scales,
-    2-D / 3-D, NaN, recover_nans)."""
-    import xcube_resampling_amd.affine as A
-    from oracle import affine_ref
-
-    monkeypatch.setenv("XRS_AFFINE_STAGE", stage)
-    for seed in range(8):
-        rng = np.random.default_rng(7000 + seed)
-        dtype = [np.float32, np.float64, np.int16, np.uint8][seed % 4]
-        nd = 3 if seed % 2 else 2
-        a = _random_case(rng, dtype, nd, 0.02)
-        s_i = float(rng.choice([2.0, 2.5, 4.0, 3.0]))
-        s_j = float(rng.choice([2.0, 3.0, 4.0, 1.5]))
-        m = ((s_i, 0.0, float(rng.uniform(-2, 2))), (0.0, s_j, float(rng.choice([0.0, 0.5]))))
-        lead = a.shape[:-2]
-        oshape = lead + (int(rng.integers(5, 30)), int(rng.integers(5, 30)))
-        ochunks = tuple(1 for _ in lead) + (int(rng.integers(4, 16)), int(rng.integers(4, 16)))
-        fill = np.nan if np.issubdtype(dtype, np.floating) else 7
-        agg = ["mean", "sum", "max", "min", "count", "prod"][seed % 6]
-        recover = bool(seed % 3 == 0 and np.issubdtype(dtype, np.floating))
-        ref = affine_ref.resample_array(a, m, oshape, ochunks, 1, agg, recover, fill)
-        got = A._resample_array(a, None, None, m, oshape, ochunks, 1, agg, recover, fill)
-        got = got if isinstance(got, np.ndarray) else got.cpu().numpy()
-        assert_bitwise_equal(got, np.asarray(ref), f"stage={stage} seed {seed} {agg}")
-
-
 @pytest.mark.parametrize("k3i", ["1", "0"])
 @pytest.mark.parametrize("dtype,nd", [(np.float32, 2), (np.float64, 2), (np.float32, 3),
                                       (np.float64, 3)])
-def test_integral_coarsen_k3i_matches_oracle(k3i, dtype, nd, monkeypatch):
+def test_integral_coarsen_k3i_matches_oracle(k3i, dtype, nd):
     """K3i (the integral-grid coarsen kernel: square factors 2/4/8 whose div-x
-    grid sits on source pixels) and the generic K3 (XRS_AFFINE_INTEGRAL=0) are
+    grid sits on source pixels) and the generic K3 (forced by the test-only
+    knob xrs_testing_set(XRS_TESTING_AFFINE_GENERIC, 1)) are
     both bit-exact with the oracle: order 0 and 1, integral offsets incl.
     misaligned vector starts and targets reaching past the source (cval /
     exact path at the edges), NaN / +-inf / -0.0 in the taps, the zero-weight
@@ -225,7 +197,8 @@ def test_integral_coarsen_k3i_matches_oracle(k3i, dtype, nd, monkeypatch):
     import xcube_resampling_amd.affine as A
     from oracle import affine_ref
 
-    monkeypatch.setenv("XRS_AFFINE_INTEGRAL", k3i)
+    from xcube_resampling_amd._native import testing_knob
+
     rng = np.random.default_rng(4242)
     lead = (3,) if nd == 3 else ()
     cases = [(4, (0.0, 0.0), (70, 300), (32, 128), 1, "mean"),
@@ -248,8 +221,9 @@ def test_integral_coarsen_k3i_matches_oracle(k3i, dtype, nd, monkeypatch):
         m = ((float(d), 0.0, ox), (0.0, float(d), oy))
         ochunks = tuple(1 for _ in lead) + tile
         ref = affine_ref.resample_array(a, m, lead + oshape, ochunks, order, agg, False, np.nan)
-        got = A._resample_array(a, None, None, m, lead + oshape, ochunks, order, agg, False,
-                                np.nan)
+        with testing_knob("affine_generic", 0 if k3i == "1" else 1):
+            got = A._resample_array(a, None, None, m, lead + oshape, ochunks, order, agg, False,
+                                    np.nan)
         got = got if isinstance(got, np.ndarray) else got.cpu().numpy()
         assert_bitwise_equal(got, np.asarray(ref), f"k3i={k3i} {dtype} d={d} off={ox},{oy} "
                                                    f"order={order} {agg}")

@@ -52,3 +52,17 @@ def test_compute_without_gpu_fails_loudly():
 
     with pytest.raises(NativeLibraryError, match="no HIP device"):
         require_device()
+
+
+def test_product_library_reads_no_environment():
+    """The product's numerics cannot depend on an environment variable: the
+    library imports no getenv (the test-only path knobs are an explicit ABI,
+    xrs_testing_set)."""
+    import subprocess
+
+    from xcube_resampling_amd import _native
+
+    syms = subprocess.run(["nm", "-D", "--undefined-only", _native.LIB_PATH],
+                          capture_output=True, text=True, check=True).stdout
+    assert "getenv" not in syms
+    assert "secure_getenv" not in syms

@@ -285,10 +285,10 @@ def test_device_tiling_matches_host_tiling(j_up, tile):
     assert_bitwise_equal(b.cpu().numpy(), a.cpu().numpy(), "device vs host tiles")
 
 
-def test_claim_fast_decisions_equal_exact_divisions(monkeypatch):
+def test_claim_fast_decisions_equal_exact_divisions():
     """K5a decides pixel windows and triangle hits by reciprocal
     multiplication with an exact-division fallback near every boundary; forcing
-    the exact path everywhere (XRS_RECTIFY_EXACT=1) gives the same ij image on
+    the exact path everywhere (test-only knob XRS_TESTING_RECTIFY_EXACT) gives the same ij image on
     a jittered swath with degenerate (duplicate) and NaN coordinates."""
     import torch
 
@@ -316,8 +316,10 @@ def test_claim_fast_decisions_equal_exact_divisions(monkeypatch):
     run = lambda: kernels.rectify_ij(xy[0], xy[1], tiles, ntx, tgm.height, tgm.width,  # noqa
                                      tgm.x_res, -tgm.y_res, 1e-3).cpu().numpy()
     fast = run()
-    monkeypatch.setenv("XRS_RECTIFY_EXACT", "1")
-    exact = run()
+    from xcube_resampling_amd._native import testing_knob
+
+    with testing_knob("rectify_exact", 1):
+        exact = run()
     assert_bitwise_equal(fast, exact, "fast vs exact decisions")
     assert np.isfinite(fast).sum() > 0.5 * fast.size
 
@@ -356,3 +358,33 @@ def test_config4_full_size_matches_oracle():
         exp = rectify_ref.compute_var_image(exp_ij, var, np.nan, interp, tile, threads=16)
         assert_bitwise_equal(kernels.rectify_var(ij, src, interp, np.nan).cpu().numpy(), exp,
                              interp)
+
+
+def test_nan_cornered_quads_on_untiled_large_target():
+    """A NaN source coordinate makes the quads that have it as corner p0 / p3
+    span their whole tile (floor(NaN) -> INT64_MIN clamps to 0,
+    rectify.py:500-526) and test only the other triangle.  On an untiled
+    ~9 Mpx target (the reference's default tiling for numpy swaths) each such
+    window holds millions of (quad, pixel) tests: K5's test numbering (int64
+    prefix sums) and (row, column) decomposition must stay exact there.  ij
+    == the C oracle bit for bit."""
+    w, h = 1600, 1400
+    jj, ii = np.mgrid[0:h, 0:w].astype(np.float64)
+    lon = 10.0 + 0.002 * ii + 0.0004 * jj
+    lat = 50.0 - 0.002 * jj + 0.0003 * ii
+    for j, i in [(1390, 1590), (1395, 20), (700, 1500)]:
+        lat[j, i] = np.nan
+    res = 0.001
+    x0 = float(np.floor(np.nanmin(lon) / res) * res)
+    y0 = float(np.floor(np.nanmin(lat) / res) * res)
+    size = (int(np.ceil((np.nanmax(lon) - x0) / res)), int(np.ceil((np.nanmax(lat) - y0) / res)))
+    assert size[0] * size[1] >= 8_500_000
+    from oracle import gridmapping_ref as gref
+
+    geo = gref.regular_geometry(size, (x0, y0), res, tile_size=size)
+    exp_ij, exp_bb = rectify_ref.compute_target_source_ij(lon, lat, size, size, geo["xy_bbox"],
+                                                          geo["xy_res"], False)
+    ij, bb = _device_ij(lon, lat, size, size, (x0, y0), res, False)
+    np.testing.assert_array_equal(bb, exp_bb)
+    assert_bitwise_equal(ij.cpu().numpy(), exp_ij, "ij")
+    assert np.isfinite(exp_ij[0]).sum() > 0.5 * size[0] * size[1]

@@ -29,18 +29,94 @@ def _plan(g):
                                                                   always_xy=True))
 
 
+@pytest.mark.parametrize("balance", ["rows", "bytes"])
 @pytest.mark.parametrize("world", [1, 2, 3, 4, 8])
-def test_band_shards_partition_target_rows(world):
+def test_band_shards_partition_target_rows(world, balance):
+    """Row-granular bands cover every target row once; each band's source
+    rows are exactly the rows its floor / ceil taps read (a superset of every
+    row K1 touches, and inside the tile windows)."""
     from xcube_resampling_amd.sharding import band_shard
 
     plan = _plan(load_golden("reproject_f32.npz"))
-    shards = [band_shard(plan, world, r) for r in range(world)]
+    shards = [band_shard(plan, world, r, balance) for r in range(world)]
     rows = [r for s in shards for r in range(s.row0, s.row1)]
     assert rows == list(range(plan.dst_height))
+    lo, hi = plan.row_source_extent()
     for s in shards:
         if s.row1 > s.row0:
-            assert s.row0 % plan.tile_height == 0
-            assert (s.src_row0, s.src_row1) == plan.source_rows_for(s.row0, s.row1)
+            ok = hi[s.row0:s.row1] >= lo[s.row0:s.row1]
+            if not ok.any():   # the band reads only padding (fill)
+                assert s.src_rows == (0, 0)
+                continue
+            assert s.src_row0 == lo[s.row0:s.row1][ok].min()
+            assert s.src_row1 == hi[s.row0:s.row1][ok].max() + 1
+            w0, w1 = plan.source_rows_for(s.row0, s.row1)
+            assert w0 <= s.src_row0 and s.src_row1 <= w1
+
+
+def test_row_extents_match_oracle_taps():
+    """plan.row_source_extent == the rows the oracle's _reproject_block reads
+    (floor / ceil window indices of reproject.py:286-291 mapped through the
+    oracle's windows)."""
+    import math
+
+    from oracle import gridmapping_ref as gref
+    from oracle import reproject_ref
+
+    g = load_golden("reproject_pad.npz")
+    plan = _plan(g)
+    tsize = tuple(int(v) for v in g["tsize"])
+    ttile = tuple(int(v) for v in g["ttile"])
+    geo = gref.regular_geometry(tsize, tuple(g["txy_min"]), tuple(g["tres"]), tile_size=ttile)
+    ntx, nty = math.ceil(tsize[0] / ttile[0]), math.ceil(tsize[1] / ttile[1])
+    h, w = g["data"].shape[1:]
+    b, _, yc, pad = reproject_ref.get_scr_bboxes_indices(
+        lambda *bb: gref.transform_bounds(gref.webmerc_inverse, *bb), g["src_lon"], g["src_lat"],
+        float(g["x_res"]), float(g["y_res"]), w, h, geo["xy_bboxes"], ntx, nty)
+    lo, hi = plan.row_source_extent()
+    for r in range(tsize[1]):
+        j = r // ttile[1]
+        rows = set()
+        for i in range(ntx):
+            _, sy = gref.webmerc_inverse(geo["x_coords"][:1], geo["y_coords"][r:r + 1])
+            iy = (sy[0] - yc[0, j, i]) / -float(g["y_res"])
+            for f in (np.floor, np.ceil):
+                wi = int(np.int16(f(iy)))
+                wi = wi + yc.shape[0] if wi < 0 else wi
+                gj = int(b[1, j, i]) - pad[1][0] + wi
+                if 0 <= wi < yc.shape[0] and 0 <= gj < h:
+                    rows.add(gj)
+        if rows:
+            assert (lo[r], hi[r]) == (min(rows), max(rows)), r
+        else:
+            assert lo[r] > hi[r]
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_config5_band_balance(world):
+    """Config 5 (40960^2, 20 tile rows) split over `world` ranks at row
+    granularity: balance="rows" gives equal target rows (max/mean 1.0; whole
+    tile rows would give 1.2 at world 8), balance="bytes" equal algorithmic
+    bytes within 5 %; every source row a band holds is one it reads."""
+    import bench
+    from xcube_resampling_amd.sharding import band_shard
+
+    _, _, plan, _, _ = bench.workload(40960, 2048)
+    cols = plan.source_cols_read()
+    for balance in ("rows", "bytes"):
+        shards = [band_shard(plan, world, r, balance) for r in range(world)]
+        nrows = np.array([s.row1 - s.row0 for s in shards], float)
+        alg = np.array([4 * 40960 * (s.row1 - s.row0) + 4 * cols * (s.src_row1 - s.src_row0)
+                        for s in shards], float)
+        if balance == "rows":
+            assert nrows.max() / nrows.mean() <= 1.0 + 1e-9
+        else:
+            assert alg.max() / alg.mean() <= 1.05, alg / alg.mean()
+        assert sum(nrows) == 40960
+        # source bands are contiguous and overlap their neighbours by at most
+        # the rows two adjacent target rows share
+        for a, b in zip(shards, shards[1:]):
+            assert b.src_row0 >= a.src_row0 and a.src_row1 - b.src_row0 <= 2
 
 
 @pytest.mark.parametrize("n,world", [(1, 1), (8, 8), (5, 2), (3, 4), (17, 8)])
@@ -57,7 +133,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _rank_main(rank, world, port, result_dir):
+def _rank_main(rank, world, port, result_dir, balance="rows"):
     import sys
 
     import torch
@@ -76,7 +152,7 @@ def _rank_main(rank, world, port, result_dir):
     try:
         g = load_golden("reproject_f32.npz")
         plan = _plan(g)
-        shard = band_shard(plan, world, rank)
+        shard = band_shard(plan, world, rank, balance)
         # the rank holds only its source rows: everything else is poison
         data = np.full_like(g["data"], POISON)
         j0, j1 = shard.src_rows
@@ -97,20 +173,25 @@ def _rank_main(rank, world, port, result_dir):
         out = gather_rows(local, plan.dst_height)
         clock = max_over_ranks(1.0 + rank)
         if rank == 0:
-            np.save(os.path.join(result_dir, "bands.npy"), out.numpy())
+            np.save(os.path.join(result_dir, f"bands_{balance}.npy"), out.numpy())
             with open(os.path.join(result_dir, "clock.txt"), "w") as f:
                 f.write(repr(clock))
     finally:
         dist.destroy_process_group()
 
 
-def test_gloo_band_sharded_reprojection_matches_reference(tmp_path):
+@pytest.mark.parametrize("balance", ["rows", "bytes"])
+def test_gloo_band_sharded_reprojection_matches_reference(tmp_path, balance):
+    """world_size 2 over gloo: each rank holds only the source rows of its
+    row band (everything else poisoned), bands split mid-tile, and the
+    gathered raster equals the reference's output bit for bit."""
     import torch.multiprocessing as mp
 
     world = 2
-    mp.spawn(_rank_main, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    mp.spawn(_rank_main, args=(world, _free_port(), str(tmp_path), balance), nprocs=world,
+             join=True)
     g = load_golden("reproject_f32.npz")
-    got = np.load(tmp_path / "bands.npy")
+    got = np.load(tmp_path / f"bands_{balance}.npy")
     assert got.dtype == np.float64
     np.testing.assert_array_equal(got.view(np.uint64), g["out_bilinear"].view(np.uint64))
     assert float((tmp_path / "clock.txt").read_text()) == float(world)

@@ -99,9 +99,32 @@ _SIGNATURES = {
     "xrs_rectify_tiles": (_c_int, [_c_ptr, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64,
                                    _c_i64, _c_i64, _c_i64, _c_dbl, _c_dbl, _c_dbl, _c_dbl,
                                    _c_dbl, _c_int, _c_ptr, _c_ptr, _c_ptr]),
+    "xrs_testing_set": (_c_i64, [_c_int, _c_i64]),
     "xrs_rectify_var": (_c_int, [_c_ptr, _c_i64, _c_i64, _c_ptr, _c_int, _c_i64, _c_i64, _c_i64,
                                  _c_i64, _c_i64, _c_ptr, _c_i64, _c_int, _c_dbl, _c_ptr]),
 }
+
+TESTING_KNOBS = {"reproject_band": 1, "reproject_blocks_per_cu": 2, "affine_generic": 3,
+                 "rectify_exact": 4}
+
+
+class testing_knob:
+    """Context manager forcing one test-only path knob (xrs_testing_set):
+    ``with testing_knob("rectify_exact", 1): ...``.  Tests only."""
+
+    def __init__(self, name: str, value: int):
+        self.knob = TESTING_KNOBS[name]
+        self.value = int(value)
+        self.prev = None
+
+    def __enter__(self):
+        self.prev = lib().xrs_testing_set(self.knob, self.value)
+        return self
+
+    def __exit__(self, *exc):
+        lib().xrs_testing_set(self.knob, self.prev)
+        return False
+
 
 AGG_CODES = {"mean": 1, "sum": 2, "max": 3, "min": 4, "prod": 5, "count": 6, "first": 7,
              "last": 8, "center": 9, "median": 10, "mode": 11, "std": 12, "var": 13}

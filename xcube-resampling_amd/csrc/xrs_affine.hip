@@ -195,21 +195,6 @@ struct Src {
   __device__ inline const T* row1(int32_t r) const { return g1 + (int64_t)r * sy; }
 };
 
-// Source access from the tile's source footprint staged in LDS (K3): rows
-// [r_lo, r_lo+nr), columns [c_lo, c_lo+nc) of slice t (and of t1), column
-// positions padded by lds_pos so lanes on consecutive intermediate columns
-// hit distinct banks.
-template <typename T>
-struct LdsSrc {
-  const T* s0;
-  const T* s1;
-  int r_lo, c_lo, pitch;
-  __device__ inline int32_t crow(int32_t g) const { return g < 0 ? 0 : g - r_lo; }
-  __device__ inline int32_t ccol(int32_t g) const;
-  __device__ inline const T* row0(int32_t r) const { return s0 + r * pitch; }
-  __device__ inline const T* row1(int32_t r) const { return s1 + r * pitch; }
-};
-
 // The source taps of one sub-sample (loaded first, evaluated later, so that
 // several sub-samples' loads are in flight together).
 template <typename T>
@@ -358,36 +343,6 @@ affine_direct_kernel(AffineArgs a, AxisChunks ay, AxisChunks ax) {
 // so the reduce pass (lane tx reads k = tx*dx + si) is bank-conflict free.
 __device__ inline int lds_pos(int k) { return k + (k >> 5); }
 
-template <typename T>
-__device__ inline int32_t LdsSrc<T>::ccol(int32_t g) const { return g < 0 ? 0 : lds_pos(g - c_lo); }
-
-// Per tile row block (kRedRows output rows) / column block (kTileW output
-// columns): the source index span [lo, hi] of every in-bounds tap of the
-// block's intermediate rows / columns (lo > hi: no source needed).
-__global__ void __launch_bounds__(kThreads)
-affine_bounds_kernel(const AxisTab* __restrict__ ytab, const AxisTab* __restrict__ xtab,
-                     int64_t ih, int64_t iw, int64_t rows_per_blk, int64_t cols_per_blk,
-                     int64_t nby, int64_t nbx, int32_t* __restrict__ yb, int32_t* __restrict__ xb) {
-  for (int64_t b = (int64_t)blockIdx.x * kThreads + threadIdx.x; b < nby + nbx;
-       b += (int64_t)gridDim.x * kThreads) {
-    const bool is_y = b < nby;
-    const int64_t k = is_y ? b : b - nby;
-    const int64_t per = is_y ? rows_per_blk : cols_per_blk;
-    const int64_t n = is_y ? ih : iw;
-    const AxisTab* tab = is_y ? ytab : xtab;
-    int32_t lo = INT32_MAX, hi = -1;
-    for (int64_t i = k * per; i < min(n, (k + 1) * per); ++i) {
-      const AxisTab e = tab[i];
-      if (e.g0 < 0) continue;
-      lo = min(lo, min(e.g0, e.g1));
-      hi = max(hi, max(e.g0, e.g1));
-    }
-    int32_t* out = is_y ? yb : xb;
-    out[2 * k] = lo;
-    out[2 * k + 1] = hi;
-  }
-}
-
 // K3 (coarsen reducers): a block owns 64 output columns x kRedRows output
 // rows.  For each group of G sub-sample rows it (A) evaluates the scipy
 // sub-samples of the whole intermediate band — lanes on consecutive
@@ -401,8 +356,8 @@ constexpr int kRedRows = kThreads / kTileW;  // 4 output rows per block
 // tile into the LDS band.  The column entry is the same for all rows
 // (hoisted), the row entries are block-uniform (scalar loads), and the taps of
 // KB rows are loaded before any is consumed (memory-level parallelism).
-template <typename T, typename I, int ORDER, bool RECOVER, bool HAS_T1, int KB, typename R>
-__device__ inline void fill_band(const AffineArgs& a, const R& p,
+template <typename T, typename I, int ORDER, bool RECOVER, bool HAS_T1, int KB>
+__device__ inline void fill_band(const AffineArgs& a, const Src<T>& p,
                                  const AxisTab* __restrict__ ytab,
                                  const AxisTab* __restrict__ xtab, I* buf, int64_t oj0,
                                  int64_t ic0, int rows, int s0, int g_n, int kmax,
@@ -418,7 +373,7 @@ __device__ inline void fill_band(const AffineArgs& a, const R& p,
 #pragma unroll
         for (int q = 0; q < KB; ++q) {
           ey[q] = yrow[min(g0 + q, g_n - 1)];
-          tp[q].template load<ORDER, HAS_T1, R>(p, ey[q], ex);
+          tp[q].template load<ORDER, HAS_T1>(p, ey[q], ex);
         }
 #pragma unroll
         for (int q = 0; q < KB; ++q)
@@ -504,20 +459,20 @@ struct Fold<I, false> {
   }
 };
 
-template <typename T, typename I, int ORDER, bool RECOVER, int KB>
+// sub-sample rows whose taps are loaded together (2 measured fastest of 2/4/8)
+constexpr int kReduceBatch = 2;
+
+template <typename T, typename I, int ORDER, bool RECOVER>
 __global__ void __launch_bounds__(kThreads)
 affine_reduce_kernel(AffineArgs a, const AxisTab* __restrict__ ytab,
                      const AxisTab* __restrict__ xtab, int group,
-                     const int32_t* __restrict__ yb, const int32_t* __restrict__ xb,
-                     int stage_cap, int stage_bytes, const int32_t* __restrict__ nonint,
-                     int32_t nonint_limit, int64_t slow_cap) {
+                     const int32_t* __restrict__ nonint, int32_t nonint_limit,
+                     int64_t slow_cap) {
+  constexpr int KB = kReduceBatch;
   // K3i (launched before) did the work, unless its slow-pixel list overflowed
   if (nonint && *nonint <= nonint_limit && nonint[2] <= slow_cap) return;
   extern __shared__ __align__(16) unsigned char smem[];
-  T* stage0 = reinterpret_cast<T*>(smem);
-  T* stage1 = stage0 + stage_cap;
-  I* buf = reinterpret_cast<I*>(smem + stage_bytes);
-  const int wave = wave_uniform(threadIdx.x / 64), lane = threadIdx.x % 64;
+  I* buf = reinterpret_cast<I*>(smem);
   const int tx = threadIdx.x % kTileW;
   const int ty = wave_uniform(threadIdx.x / kTileW);
   const int ny = (int)a.dy, nx = (int)a.dx;
@@ -545,59 +500,11 @@ affine_reduce_kernel(AffineArgs a, const AxisTab* __restrict__ ytab,
 
     const bool two = ORDER == 1 && t1 >= 0;
 
-    // Stage the tile's source footprint (rows yb[tj], columns xb[ti]) in LDS:
-    // every element read from HBM once per tile with all of a wave's loads
-    // issued before any is stored, instead of 4 dependent global taps per
-    // sub-sample.  Tiles whose footprint exceeds the stage read globally.
-    const bool try_stage = stage_cap > 0;
-    const int r_lo = try_stage ? yb[2 * tj] : 0, r_hi = try_stage ? yb[2 * tj + 1] : -1;
-    const int c_lo = try_stage ? xb[2 * ti] : 0, c_hi = try_stage ? xb[2 * ti + 1] : -1;
-    const int nr = r_hi - r_lo + 1, nc = c_hi - c_lo + 1;
-    const int pitch = nc > 0 ? lds_pos(nc - 1) + 1 : 0;
-    const bool staged = stage_cap > 0 && nr > 0 && nc > 0 && nr * pitch <= stage_cap &&
-                        (!two || stage_bytes >= 2 * stage_cap * (int)sizeof(T));
-    LdsSrc<T> q;
-    q.s0 = stage0; q.s1 = two ? stage1 : stage0;
-    q.r_lo = r_lo; q.c_lo = c_lo; q.pitch = pitch;
-    if (staged) {
-      const int ncb = (nc + 63) / 64, ne = nr * ncb;
-      for (int e0 = wave; e0 < ne; e0 += 4 * 8) {
-        T v0[8], v1[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const int e = e0 + 4 * u;
-          const int r = e / ncb, c = (e - r * ncb) * 64 + lane;
-          if (e < ne && c < nc) {
-            const int64_t off = (int64_t)(r_lo + r) * a.src_sy + c_lo + c;
-            v0[u] = p.g0[off];
-            if (two) v1[u] = p.g1[off];
-          }
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const int e = e0 + 4 * u;
-          const int r = e / ncb, c = (e - r * ncb) * 64 + lane;
-          if (e < ne && c < nc) {
-            stage0[r * pitch + lds_pos(c)] = v0[u];
-            if (two) stage1[r * pitch + lds_pos(c)] = v1[u];
-          }
-        }
-      }
-      __syncthreads();
-    }
-
     Fold<I> fold;
     for (int s0 = 0; s0 < ny; s0 += group) {
       const int g_n = min(group, ny - s0);
       // (A) sub-samples of rows s0 .. s0+g_n-1 into the band
-      if (staged) {
-        if (two)
-          fill_band<T, I, ORDER, RECOVER, true, KB>(a, q, ytab, xtab, buf, oj0, ic0, rows, s0,
-                                                    g_n, kmax, row_stride);
-        else
-          fill_band<T, I, ORDER, RECOVER, false, KB>(a, q, ytab, xtab, buf, oj0, ic0, rows,
-                                                     s0, g_n, kmax, row_stride);
-      } else if (two) {
+      if (two) {
         fill_band<T, I, ORDER, RECOVER, true, KB>(a, p, ytab, xtab, buf, oj0, ic0, rows, s0,
                                                   g_n, kmax, row_stride);
       } else {
@@ -893,14 +800,13 @@ inline int64_t reduce_row_bytes(int64_t dx, int64_t isize) {
 // tables really are integral is known on the device only (affine_tables_kernel
 // sets `nonint`), so K3i and the generic K3 are both launched and exactly one
 // of them works (the other returns at its first instruction).
-// A/B knob: XRS_AFFINE_INTEGRAL=0 forces the generic K3.
+// xrs_testing_set(XRS_TESTING_AFFINE_GENERIC, 1) forces the generic K3 (tests).
 template <typename T, typename I, bool RECOVER>
 inline bool integral_candidate(const AffineArgs& a) {
   if (!std::is_floating_point<T>::value || !std::is_same<T, I>::value || RECOVER) return false;
   if (a.dx != a.dy || (a.dx != 2 && a.dx != 4 && a.dx != 8)) return false;
   if (sizeof(T) == 8 && a.dx == 8) return false;   // 9 rows of 8 doubles: too many registers
-  const char* knob = std::getenv("XRS_AFFINE_INTEGRAL");
-  return !(knob && std::atoi(knob) == 0);
+  return xrs_testing_value(XRS_TESTING_AFFINE_GENERIC) == 0;
 }
 
 // Broken table entries K3i still takes (each costs its pixels the exact
@@ -914,7 +820,7 @@ inline int32_t integral_limit(int64_t ih, int64_t iw) {
 
 template <typename T, typename I, int ORDER, bool RECOVER>
 int launch(const AffineArgs& a, const AxisChunks& ay, const AxisChunks& ax, AxisTab* ytab,
-           AxisTab* xtab, int32_t* yb, int32_t* xb, int32_t* nonint, hipStream_t st) {
+           AxisTab* xtab, int32_t* nonint, hipStream_t st) {
   const bool direct = a.agg == AGG_NONE || a.agg == AGG_FIRST || a.agg == AGG_LAST ||
                       a.agg == AGG_CENTER;
   const bool k3i = !direct && integral_candidate<T, I, RECOVER>(a);
@@ -982,42 +888,9 @@ int launch(const AffineArgs& a, const AxisChunks& ay, const AxisChunks& ax, Axis
   const int64_t ntiles = ntx * nty * a.nt;
   // with K3i beside it, a small grid: it only reads the flag when K3i works
   const int nb = grid_blocks(ntiles, 1, 256 * 16);
-  // stage capacity from the scale (+ taps, mirror and rounding margin); the
-  // kernel falls back to global taps for any tile whose span exceeds it
-  const char* stage_knob = std::getenv("XRS_AFFINE_STAGE");
-  // default off: staging without prefetch adds a dependent round trip per
-  // tile (config 3: 1.89 ms staged vs 0.90 ms direct, MI355X)
-  const bool use_stage = stage_knob && std::atoi(stage_knob) != 0;
-  if (use_stage) {  // per tile row / column block: source span of its taps
-    hipLaunchKernelGGL(affine_bounds_kernel, dim3(grid_blocks(nty + ntx, kThreads, 256)),
-                       dim3(kThreads), 0, st, ytab, xtab, ay.n, ax.n, kRedRows * a.dy,
-                       kTileW * a.dx, nty, ntx, yb, xb);
-    XRS_HIP_CHECK(hipGetLastError());
-  }
-  const int64_t rows_need = (int64_t)ceil((kRedRows * a.dy - 1) * fabs(ay.scale)) + 3;
-  const int64_t cols_need = (int64_t)ceil((kTileW * a.dx - 1) * fabs(ax.scale)) + 3;
-  const int64_t cap = rows_need * (cols_need + (cols_need - 1) / 32 + 1);
-  const bool two = ORDER == 1 && a.t_next != nullptr;
-  int64_t stage_bytes = ((cap * (int64_t)sizeof(T) * (two ? 2 : 1)) + 15) / 16 * 16;
-  int64_t stage_cap = cap;
-  if (!use_stage || stage_bytes + band > 64 * 1024) stage_bytes = stage_cap = 0;
-  const size_t lds = (size_t)(stage_bytes + band);
   const int32_t* flag = k3i ? nonint : nullptr;
-  // sub-sample rows whose taps are loaded together (A/B knob XRS_AFFINE_BATCH)
-  const char* knob = std::getenv("XRS_AFFINE_BATCH");
-  const int kb = knob ? std::atoi(knob) : 2;
-  if (kb == 8)
-    hipLaunchKernelGGL((affine_reduce_kernel<T, I, ORDER, RECOVER, 8>), dim3(nb), dim3(kThreads),
-                       lds, st, args, ytab, xtab, (int)group, yb, xb, (int)stage_cap,
-                       (int)stage_bytes, flag, limit, slow_cap);
-  else if (kb == 2)
-    hipLaunchKernelGGL((affine_reduce_kernel<T, I, ORDER, RECOVER, 2>), dim3(nb), dim3(kThreads),
-                       lds, st, args, ytab, xtab, (int)group, yb, xb, (int)stage_cap,
-                       (int)stage_bytes, flag, limit, slow_cap);
-  else
-    hipLaunchKernelGGL((affine_reduce_kernel<T, I, ORDER, RECOVER, 4>), dim3(nb), dim3(kThreads),
-                       lds, st, args, ytab, xtab, (int)group, yb, xb, (int)stage_cap,
-                       (int)stage_bytes, flag, limit, slow_cap);
+  hipLaunchKernelGGL((affine_reduce_kernel<T, I, ORDER, RECOVER>), dim3(nb), dim3(kThreads),
+                     (size_t)band, st, args, ytab, xtab, (int)group, flag, limit, slow_cap);
   XRS_HIP_CHECK(hipGetLastError());
   if (k3i) {
     if constexpr (std::is_floating_point<T>::value && std::is_same<T, I>::value && !RECOVER) {
@@ -1070,9 +943,9 @@ extern "C" int xrs_any_nan(const void* src, int src_dtype, int64_t n, int32_t* f
 
 extern "C" int64_t xrs_affine_workspace_size(int64_t inter_h, int64_t inter_w) {
   if (inter_h < 0 || inter_w < 0) return 0;
-  // axis tables + per row / column block source spans (<= one per entry) +
-  // the K3i flags (broken entries, time neighbour, slow count) and slow-pixel list
-  return (inter_h + inter_w) * (int64_t)(sizeof(xrs::AxisTab) + 2 * sizeof(int32_t)) + 16 +
+  // axis tables + the K3i flags (broken entries, time neighbour, slow count)
+  // and slow-pixel list
+  return (inter_h + inter_w) * (int64_t)sizeof(xrs::AxisTab) + 16 +
          xrs::slow_capacity(inter_h, inter_w) * (int64_t)sizeof(int64_t);
 }
 
@@ -1120,18 +993,16 @@ extern "C" int xrs_affine(const void* src, int src_dtype, int64_t nt, int64_t sr
   a.ytab = a.xtab = nullptr;
   AxisTab* ytab = static_cast<AxisTab*>(workspace);
   AxisTab* xtab = ytab + ih;
-  int32_t* yb = reinterpret_cast<int32_t*>(xtab + iw);
-  int32_t* xb = yb + 2 * ih;
-  int32_t* nonint = xb + 2 * iw;
+  int32_t* nonint = reinterpret_cast<int32_t*>(xtab + iw);
   hipStream_t st = static_cast<hipStream_t>(stream);
   return dispatch_dtype(src_dtype, [&](auto tag) -> int {
     using T = decltype(tag);
     if constexpr (std::is_floating_point<T>::value) {
       if (recover_nan)
-        return order ? launch<T, double, 1, true>(a, ay, ax, ytab, xtab, yb, xb, nonint, st)
-                     : launch<T, double, 0, true>(a, ay, ax, ytab, xtab, yb, xb, nonint, st);
+        return order ? launch<T, double, 1, true>(a, ay, ax, ytab, xtab, nonint, st)
+                     : launch<T, double, 0, true>(a, ay, ax, ytab, xtab, nonint, st);
     }
-    return order ? launch<T, T, 1, false>(a, ay, ax, ytab, xtab, yb, xb, nonint, st)
-                 : launch<T, T, 0, false>(a, ay, ax, ytab, xtab, yb, xb, nonint, st);
+    return order ? launch<T, T, 1, false>(a, ay, ax, ytab, xtab, nonint, st)
+                 : launch<T, T, 0, false>(a, ay, ax, ytab, xtab, nonint, st);
   });
 }

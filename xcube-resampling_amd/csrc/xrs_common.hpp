@@ -196,6 +196,8 @@ inline int grid_blocks(int64_t nwork, int per_block, int cap) {
 
 // Thread-local error message reported through xrs_last_error().
 void xrs_set_error(const char* fmt, ...);
+// Current value of a test-only path knob (xrs_testing_set, include/xrs.h).
+int64_t xrs_testing_value(int knob);
 
 #define XRS_HIP_CHECK(expr)                                                    \
   do {                                                                         \

@@ -366,7 +366,8 @@ constexpr int kQd = 12;          // doubles per staged quad: 8 corners, det_a/b,
 
 struct ClaimLds {
   double qd[kThreads / 64][kQd][64];
-  int32_t qi[kThreads / 64][5][64];   // imin, jmin, nw, key, start
+  int32_t qi[kThreads / 64][4][64];   // imin, jmin, nw, key
+  int64_t qs[kThreads / 64][64];      // exclusive start of the quad's tests
 };
 
 __global__ void __launch_bounds__(kThreads)
@@ -414,7 +415,8 @@ rectify_claim_kernel(RectArgs a) {
     Q.x3 = __shfl_down(Q.x2, 1, 64); Q.y3 = __shfl_down(Q.y2, 1, 64);
     int64_t pi1 = __shfl_down(pi0, 1, 64), pj1 = __shfl_down(pj0, 1, 64);
     int64_t pi3 = __shfl_down(pi2, 1, 64), pj3 = __shfl_down(pj2, 1, 64);
-    int32_t cnt = 0, imin32 = 0, jmin32 = 0, nw = 1;
+    int64_t cnt = 0;   // window pixels: up to a whole (untiled) target
+    int32_t imin32 = 0, jmin32 = 0, nw = 1;
     double det_a = 0.0, det_b = 0.0;
     if (valid) {
       if (lane == 63 || li + 1 >= nq_i) {      // neighbour lane is not quad (lj, li+1)
@@ -436,21 +438,24 @@ rectify_claim_kernel(RectArgs a) {
           imin32 = (int32_t)imin;
           jmin32 = (int32_t)jmin;
           nw = (int32_t)(imax - imin + 1);
-          cnt = nw * (int32_t)(jmax - jmin + 1);
+          cnt = (int64_t)nw * (jmax - jmin + 1);
         }
       }
     }
-    // wave-exclusive prefix sum of the window sizes
-    int32_t incl = cnt;
+    // wave-exclusive prefix sum of the window sizes (int64: a quad with a NaN
+    // corner spans its whole tile, rectify.py:500-526, and a tile may be a
+    // whole untiled target)
+    int64_t incl = cnt;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
-      const int32_t v = __shfl_up(incl, o, 64);
+      const int64_t v = __shfl_up(incl, o, 64);
       if (lane >= o) incl += v;
     }
-    const int32_t total = __shfl(incl, 63, 64);
+    const int64_t total = __shfl(incl, 63, 64);
     if (total == 0) continue;
     double* qd = &L.qd[wv][0][0];
     int32_t* qs = &L.qi[wv][0][0];
+    int64_t* qst = &L.qs[wv][0];
     qd[0 * 64 + lane] = Q.x0; qd[1 * 64 + lane] = Q.y0;
     qd[2 * 64 + lane] = Q.x1; qd[3 * 64 + lane] = Q.y1;
     qd[4 * 64 + lane] = Q.x2; qd[5 * 64 + lane] = Q.y2;
@@ -460,20 +465,26 @@ rectify_claim_kernel(RectArgs a) {
     qd[11 * 64 + lane] = det_b != 0.0 ? 1.0 / det_b : 0.0;
     qs[0 * 64 + lane] = imin32; qs[1 * 64 + lane] = jmin32; qs[2 * 64 + lane] = nw;
     qs[3 * 64 + lane] = (int32_t)((int64_t)qj * a.w + qi);
-    qs[4 * 64 + lane] = incl - cnt;   // exclusive start
+    qst[lane] = incl - cnt;   // exclusive start
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    for (int32_t k = lane; k < total; k += 64) {
+    for (int64_t k = lane; k < total; k += 64) {
       int32_t o = 0;                   // owner: last lane with start <= k
 #pragma unroll
       for (int step = 32; step > 0; step >>= 1)
-        if (qs[4 * 64 + o + step] <= k) o += step;
-      const int32_t local = k - qs[4 * 64 + o];
+        if (qst[o + step] <= k) o += step;
+      // (row, column) of test `local` in the owner's window of w_ columns: the
+      // float quotient is within +-1 of local / w_ (window rows < 2^22, checked
+      // by xrs_rectify_ij), the integer remainder corrects it exactly
+      const int64_t local = k - qst[o];
       const int32_t w_ = qs[2 * 64 + o];
-      const int32_t dj_ = (int32_t)(((float)local + 0.5f) / (float)w_);
-      const int32_t di = qs[0 * 64 + o] + (local - dj_ * w_);
-      const int32_t dj = qs[1 * 64 + o] + dj_;
+      int64_t q_ = (int64_t)((float)local / (float)w_);
+      int64_t r_ = local - q_ * w_;
+      if (r_ < 0) { --q_; r_ += w_; }
+      else if (r_ >= w_) { ++q_; r_ -= w_; }
+      const int32_t di = qs[0 * 64 + o] + (int32_t)r_;
+      const int32_t dj = qs[1 * 64 + o] + (int32_t)q_;
       const double x0 = qd[0 * 64 + o], y0 = qd[1 * 64 + o], x1 = qd[2 * 64 + o],
                    y1 = qd[3 * 64 + o], x2 = qd[4 * 64 + o], y2 = qd[5 * 64 + o],
                    x3 = qd[6 * 64 + o], y3 = qd[7 * 64 + o];
@@ -704,7 +715,8 @@ extern "C" int xrs_rectify_ij(const double* x, const double* y, int64_t h, int64
                               void* stream) {
   using namespace xrs;
   if (!x || !y || !tiles || !keys || !ij || h < 2 || w < 2 || sy < w || ntiles < 1 ||
-      dst_h < 1 || dst_w < 1 || h * w >= (int64_t)UINT32_MAX || !chunk_offsets || max_chunks < 0) {
+      dst_h < 1 || dst_w < 1 || h * w >= (int64_t)UINT32_MAX || !chunk_offsets || max_chunks < 0 ||
+      dst_h >= (1 << 22) || dst_w > INT32_MAX) {
     xrs_set_error("xrs_rectify_ij: invalid argument");
     return XRS_ERR_ARG;
   }
@@ -715,18 +727,15 @@ extern "C" int xrs_rectify_ij(const double* x, const double* y, int64_t h, int64
   a.dst_h = dst_h; a.dst_w = dst_w; a.x_scale = x_scale; a.y_scale = y_scale;
   a.uv_delta = uv_delta; a.keys = keys; a.ij = ij;
   a.inv_x = 1.0 / x_scale; a.inv_y = 1.0 / y_scale;
-  // A/B + test knob: XRS_RECTIFY_EXACT=1 takes the exact divisions everywhere
-  const char* ex = getenv("XRS_RECTIFY_EXACT");
-  a.margin = ex && atoi(ex) != 0 ? INFINITY : kMargin;
+  // tests: xrs_testing_set(XRS_TESTING_RECTIFY_EXACT, 1) takes the exact
+  // divisions for every decision
+  a.margin = xrs_testing_value(XRS_TESTING_RECTIFY_EXACT) != 0 ? INFINITY : kMargin;
   hipStream_t st = static_cast<hipStream_t>(stream);
   XRS_HIP_CHECK(hipMemsetAsync(keys, 0xFF, (size_t)(dst_h * dst_w) * sizeof(uint32_t), st));
   {
-    // A/B knob: XRS_RECTIFY_BLOCKS_PER_CU (0 = one chunk per block when the
-    // caller knows the chunk count, else 16 blocks per CU)
-    const char* bpc = getenv("XRS_RECTIFY_BLOCKS_PER_CU");
-    const int cap = bpc && atoi(bpc) > 0 ? 256 * atoi(bpc) : (1 << 24);
-    const int nb = max_chunks > 0 ? grid_blocks(max_chunks, 1, cap)
-                                  : grid_blocks(256 * 16, 1, cap);
+    // one chunk per block when the caller knows the chunk count, else 16 blocks per CU
+    const int nb = max_chunks > 0 ? grid_blocks(max_chunks, 1, 1 << 24)
+                                  : grid_blocks(256 * 16, 1, 1 << 24);
     const size_t lds = sizeof(ClaimLds) +
                        (ntiles <= kOffsLds ? (size_t)(ntiles + 1) * sizeof(int64_t) : 0);
     hipLaunchKernelGGL(rectify_claim_kernel, dim3(nb), dim3(kThreads), lds, st, a);

@@ -1,5 +1,6 @@
 // xrs_runtime.cpp — library identification and the thread-local error channel
 // behind xrs_last_error() (include/xrs.h).
+#include <atomic>
 #include <cstdarg>
 #include <cstdio>
 
@@ -9,6 +10,7 @@
 
 namespace {
 thread_local char g_last_error[1024] = "";
+std::atomic<int64_t> g_testing[XRS_TESTING_NUM_KNOBS];   // zero-initialised: product paths
 }
 
 void xrs_set_error(const char* fmt, ...) {
@@ -16,6 +18,18 @@ void xrs_set_error(const char* fmt, ...) {
   va_start(ap, fmt);
   std::vsnprintf(g_last_error, sizeof(g_last_error), fmt, ap);
   va_end(ap);
+}
+
+int64_t xrs_testing_value(int knob) {
+  return knob > 0 && knob < XRS_TESTING_NUM_KNOBS ? g_testing[knob].load() : 0;
+}
+
+extern "C" int64_t xrs_testing_set(int knob, int64_t value) {
+  if (knob <= 0 || knob >= XRS_TESTING_NUM_KNOBS) {
+    xrs_set_error("xrs_testing_set: unknown knob %d", knob);
+    return XRS_ERR_ARG;
+  }
+  return g_testing[knob].exchange(value);
 }
 
 extern "C" const char* xrs_version(void) { return "xrs 0.1.0 (gfx950)"; }

@@ -66,6 +66,10 @@ def reproject(src, plan, interp: str, fill: float, out_dtype=None, rows=None, ou
     if out_dtype is None:
         out_dtype = np.float64 if interp == "bilinear" else _np_dtype(src)
     r0, r1 = (0, plan.dst_height) if rows is None else rows
+    if h_band == 0:
+        # a band that reads no source row (all taps in the padding): K1 still
+        # addresses element 0 of the band for out-of-source taps
+        src = torch().zeros((n, 1, w), dtype=src.dtype, device=device)
     if out is None:
         out = empty((n, r1 - r0, plan.dst_width), out_dtype, device)
     tables = plan.device_tables(device)

@@ -95,6 +95,73 @@ class ReprojectPlan:
             self._device_cache[key] = ws
         return ws
 
+    def _row_read_grid(self):
+        """(H', ntiles_x) int64 arrays (lo, hi) of the global source rows the
+        floor / ceil taps of each target row read in each tile column
+        (reproject.py:279, 286-291, 316-321: int16 window index with
+        python-style wrap, window origin, rows outside the source read the
+        pad and are not counted); lo > hi where nothing is read."""
+        cache = self._device_cache.get("row_read_grid")
+        if cache is not None:
+            return cache
+        ntx, _ = self.num_tiles
+        rows = np.arange(self.dst_height)
+        ty = rows // self.tile_height
+        lo = np.full((self.dst_height, ntx), np.iinfo(np.int64).max, np.int64)
+        hi = np.full((self.dst_height, ntx), -1, np.int64)
+        for tx in range(ntx):
+            t = ty * ntx + tx
+            iy = (self.src_y[rows] - self.tile_y0[t].astype(np.float64)) / -self.y_res
+            for f in (np.floor, np.ceil):
+                with np.errstate(invalid="ignore"):
+                    w = f(iy).astype(np.int16).astype(np.int64)
+                w = np.where(w < 0, w + self.win_height, w)
+                g = self.tile_win[t, 1] + w
+                ok = (w >= 0) & (w < self.win_height) & (g >= 0) & (g < self.src_height)
+                lo[:, tx] = np.where(ok, np.minimum(lo[:, tx], g), lo[:, tx])
+                hi[:, tx] = np.where(ok, np.maximum(hi[:, tx], g), hi[:, tx])
+        self._device_cache["row_read_grid"] = (lo, hi)
+        return lo, hi
+
+    def row_source_extent(self) -> tuple[np.ndarray, np.ndarray]:
+        """Per target row: the lowest and highest global source row read
+        (lo > hi: none).  Separable plans only."""
+        if self.coord_mode != 0:
+            raise NotImplementedError("row extents need separable coordinate tables")
+        lo, hi = self._row_read_grid()
+        return lo.min(axis=1), hi.max(axis=1)
+
+    def source_cols_read(self) -> int:
+        """Number of distinct source columns any target pixel reads (separable
+        plans; bilinear floor + ceil taps)."""
+        ntx, nty = self.num_tiles
+        cols = np.zeros(self.src_width, bool)
+        for t in range(ntx * nty):
+            tx = t % ntx
+            c = np.arange(tx * self.tile_width, min(self.dst_width, (tx + 1) * self.tile_width))
+            ix = (self.src_x[c] - self.tile_x0[t].astype(np.float64)) / self.x_res
+            for f in (np.floor, np.ceil):
+                with np.errstate(invalid="ignore"):
+                    w = f(ix).astype(np.int16).astype(np.int64)
+                w = np.where(w < 0, w + self.win_width, w)
+                g = self.tile_win[t, 0] + w
+                ok = (w >= 0) & (w < self.win_width) & (g >= 0) & (g < self.src_width)
+                cols[g[ok]] = True
+        return int(cols.sum())
+
+    def source_rows_read(self, r0: int, r1: int) -> tuple[int, int]:
+        """Global source rows [j0, j1) that K1 reads for target rows [r0, r1)
+        — exactly (separable plans) or the union of the tile windows
+        (2-D coordinate plans)."""
+        if self.coord_mode != 0:
+            return self.source_rows_for(r0, r1)
+        lo, hi = self.row_source_extent()
+        lo, hi = lo[r0:r1], hi[r0:r1]
+        ok = hi >= lo
+        if not ok.any():
+            return 0, 0
+        return int(lo[ok].min()), int(hi[ok].max()) + 1
+
     def source_rows_for(self, r0: int, r1: int) -> tuple[int, int]:
         """Global source rows [j0, j1) read by target rows [r0, r1) (clipped)."""
         tys = range(r0 // self.tile_height, (max(r1, r0 + 1) - 1) // self.tile_height + 1)

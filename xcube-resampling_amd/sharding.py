@@ -8,12 +8,12 @@ independent task, and a dim-0 axis (time / band) maps block-wise
 a raster, so ranks split the work along the two axes that need no exchange:
 
 * ``slice_shard``  — dim-0 slices of an (n, H, W) cube; each rank owns whole
-                     rasters (weak scaling; the bench's partition);
-* ``band_shard``   — target tile rows of one raster; each rank holds only the
-                     source rows its tiles read (``ReprojectPlan.source_rows_for``)
-                     and writes disjoint target rows (strong scaling of one
-                     raster; a 40960^2 f32 source needs 6.7 GB, so this is for
-                     rasters that exceed one GPU or for latency).
+                     rasters (weak scaling; ``bench.py --shard slices``);
+* ``band_shard``   — target rows of ONE raster (row granularity, balanced by
+                     rows or by algorithmic bytes); each rank holds only the
+                     source rows its band reads (``ReprojectPlan.
+                     source_rows_read``) and writes disjoint target rows —
+                     the bench's partition of config 5 (strong scaling).
 
 Collectives appear only around the data path: ``max_over_ranks`` (the bench's
 clock) and ``gather_rows`` (assembling a result on one rank when asked).
@@ -23,6 +23,8 @@ from __future__ import annotations
 
 import os
 from dataclasses import dataclass
+
+import numpy as np
 
 
 def balanced_range(n: int, world: int, rank: int) -> tuple[int, int]:
@@ -57,17 +59,52 @@ class BandShard:
         return self.src_row0, self.src_row1
 
 
-def band_shard(plan, world: int, rank: int) -> BandShard:
-    """Target rows of `rank`, aligned to whole tile rows (so every rank runs
-    the same per-tile windows as the single-GPU launch), and the source rows
-    they read.  Ranks beyond the number of tile rows get an empty band."""
-    nty = plan.num_tiles[1]
-    t0, t1 = balanced_range(nty, world, rank)
-    r0 = min(t0 * plan.tile_height, plan.dst_height)
-    r1 = min(t1 * plan.tile_height, plan.dst_height)
+def band_splits(plan, world: int, balance: str = "rows", out_itemsize: int = 4) -> list[int]:
+    """Target-row boundaries r_0 = 0 <= r_1 <= ... <= r_world = H of a
+    `world`-way split of one raster at ROW granularity (K1 takes arbitrary
+    row bands: ``xrs_reproject(row_begin, row_end)``; SURVEY §8(e) — whole
+    tile rows give a 3/3/3/3/2/2/2/2 split of config 5's 20 tile rows).
+
+    balance="rows":  equal target rows (equal output bytes and gather work);
+    balance="bytes": equal algorithmic bytes per band (output + the distinct
+                     source rows it reads: at config 5 a target row near 30 N
+                     reads 2.6x the source rows of one near 70 N)."""
+    h = plan.dst_height
+    if world < 1:
+        raise ValueError(f"invalid world size {world}")
+    if balance == "rows":
+        return [balanced_range(h, world, r)[0] for r in range(world)] + [h]
+    if balance != "bytes":
+        raise ValueError(f"balance must be 'rows' or 'bytes', was {balance!r}")
+    lo, hi = plan.row_source_extent()
+    cols = plan.source_cols_read()
+    valid = hi >= lo
+    # cumulative bytes F(r) of target rows [0, r): output rows + distinct
+    # source rows (source rows grow monotonically with target rows here; the
+    # running max of the last row read bounds them)
+    first = int(lo[valid].min()) if valid.any() else 0
+    run_hi = np.maximum.accumulate(np.where(valid, hi, first - 1))
+    src_rows = np.concatenate([[0], np.maximum(run_hi - first + 1, 0)])
+    f = out_itemsize * plan.dst_width * np.arange(h + 1) + 4 * cols * src_rows
+    targets = f[-1] * np.arange(1, world) / world
+    cuts = np.searchsorted(f, targets, side="left")
+    return [0] + [int(c) for c in cuts] + [h]
+
+
+def band_shard(plan, world: int, rank: int, balance: str = "rows",
+               out_itemsize: int = 4) -> BandShard:
+    """Target rows of `rank` in a row-granular split of one raster
+    (``band_splits``) and the global source rows they read
+    (``ReprojectPlan.source_rows_read``: exactly the rows K1 touches, so a
+    device holds nothing more).  Ranks beyond the number of rows get an
+    empty band."""
+    if not 0 <= rank < world:
+        raise ValueError(f"invalid rank {rank} for world size {world}")
+    cuts = band_splits(plan, world, balance, out_itemsize)
+    r0, r1 = cuts[rank], cuts[rank + 1]
     if r1 <= r0:
         return BandShard(rank, world, r0, r0, 0, 0)
-    j0, j1 = plan.source_rows_for(r0, r1)
+    j0, j1 = plan.source_rows_read(r0, r1)
     return BandShard(rank, world, r0, r1, j0, j1)
 
 
