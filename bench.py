@@ -82,7 +82,7 @@ def source_pixels_read(plan, band=None) -> int:
         for idx, base, n, mask in ((ix, plan.tile_win[t, 0], plan.src_width, cols),
                                    (iy, plan.tile_win[t, 1], plan.src_height, rows)):
             for f in (np.floor, np.ceil):
-                g = base + f.astype(np.int64)
+                g = base + f(idx).astype(np.int64)
                 g = g[(g >= 0) & (g < n)]
                 mask[g] = True
     return int(rows.sum()) * int(cols.sum())
@@ -213,8 +213,9 @@ def main():
                     help="bands: the ranks split the target rows of ONE raster, each holding "
                          "only the source rows its band reads (strong; configs[4]); "
                          "slices: rank r reprojects its own raster (weak)")
-    ap.add_argument("--balance", choices=["rows", "bytes"], default="rows",
-                    help="row-band split: equal target rows or equal algorithmic bytes")
+    ap.add_argument("--balance", choices=["rows", "bytes", "cost"], default="rows",
+                    help="row-band split: equal target rows, equal algorithmic bytes, or "
+                         "equal measured K1 cost (sharding.band_splits)")
     args = ap.parse_args()
 
     from xcube_resampling_amd.sharding import band_shard, env_rank, max_over_ranks

@@ -8,8 +8,8 @@ job's time — without an 8-GPU node.
 
     python scripts/rehearse_bands.py [--worlds 1 2 4 8] [--balance rows bytes]
 
-Prints one JSON line per (world, balance): per-rank ms (HIP events, median
-of --reps launches), max/mean, and the strong-scaling projection
+Prints one JSON line per (world, balance): per-rank ms (HIP events around
+--reps back-to-back launches, median of 5), max/mean, and the strong-scaling projection
 value = 40960^2 / max rank time.
 """
 import argparse
@@ -27,7 +27,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--size", type=int, default=40960)
     ap.add_argument("--worlds", type=int, nargs="+", default=[1, 2, 4, 8])
-    ap.add_argument("--balance", nargs="+", default=["rows", "bytes"])
+    ap.add_argument("--balance", nargs="+", default=["rows", "cost"])
     ap.add_argument("--reps", type=int, default=15)
     a = ap.parse_args()
 
@@ -54,17 +54,20 @@ def main():
                                                 out_dtype=np.float32, out=out, rows=sh.rows,
                                                 src_row0=j0, flags=flags, check=False)
                 run()
+                torch.cuda.synchronize()
+                # back-to-back launches between two events (the host's launch
+                # latency is hidden, as in the bench's graph replay); median of 5
                 times = []
-                for _ in range(a.reps):
+                for _ in range(5):
                     e0 = torch.cuda.Event(enable_timing=True)
                     e1 = torch.cuda.Event(enable_timing=True)
                     e0.record()
-                    run()
+                    for _ in range(a.reps):
+                        run()
                     e1.record()
                     e1.synchronize()
-                    times.append(e0.elapsed_time(e1))
+                    times.append(e0.elapsed_time(e1) / a.reps)
                 flags.raise_if_set("rehearsal")
-                ref = full[:, :0]  # noqa: F841
                 ranks.append(dict(rank=r, rows=[sh.row0, sh.row1], src_rows=[j0, j1],
                                   ms=round(float(np.median(times)), 4)))
                 del src, out

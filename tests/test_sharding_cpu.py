@@ -29,7 +29,7 @@ def _plan(g):
                                                                   always_xy=True))
 
 
-@pytest.mark.parametrize("balance", ["rows", "bytes"])
+@pytest.mark.parametrize("balance", ["rows", "bytes", "cost"])
 @pytest.mark.parametrize("world", [1, 2, 3, 4, 8])
 def test_band_shards_partition_target_rows(world, balance):
     """Row-granular bands cover every target row once; each band's source
@@ -97,21 +97,29 @@ def test_config5_band_balance(world):
     """Config 5 (40960^2, 20 tile rows) split over `world` ranks at row
     granularity: balance="rows" gives equal target rows (max/mean 1.0; whole
     tile rows would give 1.2 at world 8), balance="bytes" equal algorithmic
-    bytes within 5 %; every source row a band holds is one it reads."""
+    bytes within 5 %, balance="cost" equal modelled K1 time within 1 %
+    (model fitted to the one-GPU rehearsal); every source row a band holds is
+    one it reads."""
     import bench
     from xcube_resampling_amd.sharding import band_shard
 
     _, _, plan, _, _ = bench.workload(40960, 2048)
     cols = plan.source_cols_read()
-    for balance in ("rows", "bytes"):
+    from xcube_resampling_amd.sharding import COST_SRC_ROW_WEIGHT
+
+    for balance in ("rows", "bytes", "cost"):
         shards = [band_shard(plan, world, r, balance) for r in range(world)]
         nrows = np.array([s.row1 - s.row0 for s in shards], float)
         alg = np.array([4 * 40960 * (s.row1 - s.row0) + 4 * cols * (s.src_row1 - s.src_row0)
                         for s in shards], float)
+        cost = np.array([(s.row1 - s.row0) + COST_SRC_ROW_WEIGHT * (s.src_row1 - s.src_row0)
+                         for s in shards])
         if balance == "rows":
             assert nrows.max() / nrows.mean() <= 1.0 + 1e-9
-        else:
+        elif balance == "bytes":
             assert alg.max() / alg.mean() <= 1.05, alg / alg.mean()
+        else:
+            assert cost.max() / cost.mean() <= 1.01, cost / cost.mean()
         assert sum(nrows) == 40960
         # source bands are contiguous and overlap their neighbours by at most
         # the rows two adjacent target rows share

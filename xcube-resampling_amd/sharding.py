@@ -59,6 +59,12 @@ class BandShard:
         return self.src_row0, self.src_row1
 
 
+# K1 time per band on MI355X ~ rows + COST_SRC_ROW_WEIGHT x source rows read
+# (least-squares fit over the per-rank kernel times of the one-GPU rehearsal
+# of 1/2/4/8-way splits of config 5: profiles/r02_band_rehearsal.jsonl)
+COST_SRC_ROW_WEIGHT = 0.147
+
+
 def band_splits(plan, world: int, balance: str = "rows", out_itemsize: int = 4) -> list[int]:
     """Target-row boundaries r_0 = 0 <= r_1 <= ... <= r_world = H of a
     `world`-way split of one raster at ROW granularity (K1 takes arbitrary
@@ -68,24 +74,30 @@ def band_splits(plan, world: int, balance: str = "rows", out_itemsize: int = 4) 
     balance="rows":  equal target rows (equal output bytes and gather work);
     balance="bytes": equal algorithmic bytes per band (output + the distinct
                      source rows it reads: at config 5 a target row near 30 N
-                     reads 2.6x the source rows of one near 70 N)."""
+                     reads 2.6x the source rows of one near 70 N);
+    balance="cost":  equal measured K1 time: rows + COST_SRC_ROW_WEIGHT x
+                     source rows (the gather is bound by target pixels more
+                     than by source bytes: equal bytes over-corrects)."""
     h = plan.dst_height
     if world < 1:
         raise ValueError(f"invalid world size {world}")
     if balance == "rows":
         return [balanced_range(h, world, r)[0] for r in range(world)] + [h]
-    if balance != "bytes":
-        raise ValueError(f"balance must be 'rows' or 'bytes', was {balance!r}")
+    if balance == "bytes":
+        row_w, src_w = out_itemsize * plan.dst_width, 4 * plan.source_cols_read()
+    elif balance == "cost":
+        row_w, src_w = 1.0, COST_SRC_ROW_WEIGHT
+    else:
+        raise ValueError(f"balance must be 'rows', 'bytes' or 'cost', was {balance!r}")
     lo, hi = plan.row_source_extent()
-    cols = plan.source_cols_read()
     valid = hi >= lo
-    # cumulative bytes F(r) of target rows [0, r): output rows + distinct
-    # source rows (source rows grow monotonically with target rows here; the
-    # running max of the last row read bounds them)
+    # cumulative cost F(r) of target rows [0, r): rows + distinct source rows
+    # (source rows grow monotonically with target rows here; the running max
+    # of the last row read bounds them)
     first = int(lo[valid].min()) if valid.any() else 0
     run_hi = np.maximum.accumulate(np.where(valid, hi, first - 1))
     src_rows = np.concatenate([[0], np.maximum(run_hi - first + 1, 0)])
-    f = out_itemsize * plan.dst_width * np.arange(h + 1) + 4 * cols * src_rows
+    f = row_w * np.arange(h + 1) + src_w * src_rows
     targets = f[-1] * np.arange(1, world) / world
     cuts = np.searchsorted(f, targets, side="left")
     return [0] + [int(c) for c in cuts] + [h]
