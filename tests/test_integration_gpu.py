@@ -20,7 +20,7 @@ def _stub_namespace():
     import xcube_resampling_amd._native as N
 
     text = open(os.path.join(ROOT, "INTEGRATION.md")).read()
-    code = re.findall(r"```python\n(.*?)```", text, re.S)[0]
+    code = re.findall(r"```python\n(.*?)```", text, re.S)[0]   # the first block: the stub
     code = code.replace('"/path/to/libxrs.so"', repr(N.LIB_PATH))
     ns: dict = {}
     exec(compile(code, "INTEGRATION.md", "exec"), ns)
@@ -49,3 +49,29 @@ def test_integration_stub_matches_reference(interp):
                               (plan.tile_height, plan.tile_width),
                               (plan.dst_height, plan.dst_width), plan.x_res, plan.y_res,
                               "cubic", np.nan)
+
+
+@pytest.mark.parametrize("case", ["f32", "u8", "i16", "pad"])
+@pytest.mark.parametrize("interp", ["nearest", "bilinear", "triangular"])
+def test_integration_stub_on_reference_window_outputs(case, interp):
+    """INTEGRATION.md's mapping driven by the REFERENCE's own window outputs:
+    the golden fixtures hold what _get_scr_bboxes_indices returned
+    (scr_ij_bboxes, x_coords, y_coords, pad_width, reproject.py:385-469);
+    tables_from_windows maps them onto the ABI tables, the target centres are
+    transformed per column / row by the oracle, and the stub reproduces the
+    reference's blocks bit for bit."""
+    from oracle import gridmapping_ref as gref
+
+    ns = _stub_namespace()
+    g = load_golden(f"reproject_{case}.npz")
+    tx0, ty0, twin, win_hw = ns["tables_from_windows"](g["scr_ij_bboxes"], g["x_coords"],
+                                                        g["y_coords"], g["pad_width"])
+    tsize = tuple(int(v) for v in g["tsize"])
+    ttile = tuple(int(v) for v in g["ttile"])
+    geo = gref.regular_geometry(tsize, tuple(g["txy_min"]), tuple(g["tres"]), tile_size=ttile)
+    sx, _ = gref.webmerc_inverse(geo["x_coords"], np.zeros(tsize[0]))
+    _, sy = gref.webmerc_inverse(np.zeros(tsize[1]), geo["y_coords"])
+    out = ns["reproject_tiles"](g["data"], sx, sy, tx0, ty0, twin, win_hw,
+                                (ttile[1], ttile[0]), (tsize[1], tsize[0]), float(g["x_res"]),
+                                float(g["y_res"]), interp, g["fill"].item())
+    assert_bitwise_equal(out, g[f"out_{interp}"], f"{case}/{interp}")
