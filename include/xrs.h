@@ -241,11 +241,12 @@ int xrs_ij_bboxes(const double* x, const double* y, int64_t h, int64_t w, int64_
  *   swin, shin; float64 x_off, y_off} (row-major, ntiles_x per row): target
  *   tile origin/size, source window origin (si0 = -1: no source) and size,
  *   and the reference's per-tile dst_x/y_offset.
- * chunk_offsets (device, ntiles + 1): the work list of 256-quad chunks as
- *   an exclusive prefix sum of each tile's chunk count (ceil((swin-1)*(shin-1)
- *   / 256)); chunk_offsets[ntiles] = total.  Produced by xrs_rectify_tiles on
+ * chunk_offsets (device, ntiles + 1): the work list of quad strips (16
+ *   quad rows x 63 quads, one wave each) as an exclusive prefix sum of each
+ *   tile's strip count (ceil((swin-1)/63) * ceil((shin-1)/16), 0 for a tile
+ *   without source); chunk_offsets[ntiles] = total.  Produced by xrs_rectify_tiles on
  *   the device, so no host round trip is needed between K4 and K5.
- * max_chunks: the total if the caller knows it (one chunk per block), else 0
+ * max_chunks: the total if the caller knows it (one strip per wave), else 0
  *   (a persistent grid reads the total on the device).
  * x_scale = dst_x_res; y_scale = dst_y_res (j-axis up) or -dst_y_res.
  * keys: (dst_h, dst_w) uint32 scratch; ij: (2, dst_h, dst_w) float64 output

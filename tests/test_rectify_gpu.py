@@ -274,9 +274,10 @@ def test_device_tiling_matches_host_tiling(j_up, tile):
     tiles, ntx, _, _ = R.rectify_tiles(sgm, tgm, xy=xy)
     t_dev, offs = R._device_tiles(sgm, tgm, xy)
     assert np.array_equal(t_dev.cpu().numpy(), tiles.view(np.uint8).ravel())
-    nq = np.where(tiles["si0"] >= 0, np.maximum(tiles["swin"] - 1, 0).astype(np.int64)
-                  * np.maximum(tiles["shin"] - 1, 0), 0)
-    exp_offs = np.concatenate([[0], np.cumsum((nq + 255) // 256)])
+    nqi = np.maximum(tiles["swin"] - 1, 0).astype(np.int64)
+    nqj = np.maximum(tiles["shin"] - 1, 0).astype(np.int64)
+    nch = np.where(tiles["si0"] >= 0, (nqi + 62) // 63 * ((nqj + 15) // 16), 0)
+    exp_offs = np.concatenate([[0], np.cumsum(nch)])
     np.testing.assert_array_equal(offs.cpu().numpy(), exp_offs)
     ysc = tgm.y_res if j_up else -tgm.y_res
     a = kernels.rectify_ij(xy[0], xy[1], tiles, ntx, tgm.height, tgm.width, tgm.x_res, ysc, 1e-3)

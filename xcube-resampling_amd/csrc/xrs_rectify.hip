@@ -32,6 +32,8 @@ namespace xrs {
 namespace {
 
 constexpr int kThreads = 256;
+constexpr int kStripW = 63;   // K5a strip: quads per row (64 point columns = one wave)
+constexpr int kStripH = 16;   // K5a strip: quad rows
 
 // ---- wave-level helpers (64 lanes) ------------------------------------------
 __device__ inline int32_t wave_min(int32_t v) {
@@ -247,12 +249,13 @@ struct RectArgs {
   int64_t h, w, sy;
   const TileInfo* tiles;
   int64_t ntiles;
-  const int64_t* chunk_offs;   // (ntiles + 1): first 256-quad chunk of each tile
+  const int64_t* chunk_offs;   // (ntiles + 1): first quad strip of each tile
   int64_t dst_h, dst_w;
   double x_scale, y_scale;     // dst_x_res, dst_y_res (negated when j-axis down)
   double uv_delta;
   double inv_x, inv_y;         // 1 / x_scale, 1 / y_scale (claim fast paths)
-  double margin;               // relative decision margin (inf: always exact)
+  double margin;               // window floors: relative margin (inf: always exact)
+  double uv_margin;            // triangle tests: margin in u units (inf: always exact)
   uint32_t* keys;              // (dst_h, dst_w) claim keys, 0xFFFFFFFF = free
   double* ij;                  // (2, dst_h, dst_w) output
 };
@@ -302,15 +305,6 @@ __device__ inline void quad_dets(const Quad& q, double& det_a, double& det_b) {
   if (det_b != det_b) det_b = 0.0;
 }
 
-// target pixel (column, row) of a source point relative to a tile, as
-// np.floor(...).astype(np.int64) (rectify.py:500-501)
-__device__ inline int64_t pix_i(const RectArgs& a, const TileInfo& ti, double x) {
-  return f64_to_i64_x86(floor((x - ti.x_off) / a.x_scale));
-}
-__device__ inline int64_t pix_j(const RectArgs& a, const TileInfo& ti, double y) {
-  return f64_to_i64_x86(floor((y - ti.y_off) / a.y_scale));
-}
-
 // ---- division-free decisions with an exact fallback (K5a) ---------------------
 // K5a only needs the integer pixel window of each corner and the hit / no-hit
 // decision of each triangle.  Both are taken from a multiplication by the
@@ -321,62 +315,139 @@ __device__ inline int64_t pix_j(const RectArgs& a, const TileInfo& ti, double y)
 // path).  K5b recomputes the winner with the exact divisions.
 constexpr double kMargin = 1e-9;
 
-__device__ inline int64_t pix_fast(double x, double off, double scale, double inv,
-                                   double margin) {
-  const double d = x - off;
-  const double q = d * inv;
-  const double fq = floor(q);
-  const double m = margin * (1.0 + fabs(q));
-  if (q - fq > m && (fq + 1.0) - q > m) return f64_to_i64_x86(fq);
-  return f64_to_i64_x86(floor(d / scale));
-}
+// ---- K5a: claim target pixels with the raster-order key of hitting quads -------
+// Work item ("strip") = kStripH quad rows x kStripW quads of one tile's source
+// window, walked by ONE wave: lane l owns point column l of the strip (64
+// points = 63 quads), so each source point is loaded and scaled to target
+// pixel units once per strip row; the quad to its right takes the right-hand
+// corners from the next lane (DPP wave shift) and, walking down, a row's
+// bottom corners become the next row's top corners in registers.
+//
+// Window.  The reference tests every pixel of the window spanned by the
+// floors of the four corners' pixel coordinates (rectify.py:500-526); floor is
+// monotone, so the window comes from the extreme corners: two floors per axis,
+// taken by the reciprocal when clearly (relative margin) away from an integer,
+// else from the reference's per-corner divisions.
+//
+// Tests.  Per triangle (A = p0 p1 p2, B = p3 p2 p1) the reference computes
+// nu = _fu(...), nv = _fv(...) (rectify.py:737-768), u = nu / det, v = nv /
+// det and hits when u >= umin, v >= umin, u + v <= uvmax.  The quad hoists
+// the corner differences inside _fdet / _fu / _fv (the same float64
+// operations, so det and every numerator are bit-identical to the
+// reference's) and walks its clipped window in its own lane; u and v come
+// from the reciprocal of det when clearly (kUvMargin) away from every limit,
+// else from the reference's divisions, so every hit / miss equals the
+// reference's.  Hits are claimed with a global atomicMin of the quad's key.
+//
+// Windows larger than kLaneWindow (a quad with a NaN corner spans its whole
+// tile, rectify.py:500-526) are walked by the whole wave, 64 pixels per step,
+// with the reference's exact test.  Strips are independent (no block
+// synchronisation after the offsets are staged).
+// Work list: chunk c belongs to the tile t with offs[t] <= c < offs[t+1] (the
+// offsets come from xrs_rectify_tiles on the device, or from the host).
+constexpr int kOffsLds = 2047;   // tiles whose offsets are copied to LDS (16 KB)
+constexpr int kLaneWindow = 16;  // windows up to this many pixels: walked per lane
+constexpr double kUvMargin = 1e-9;
 
-// triangle test of rectify.py:556-573 (u from fu over the (p0, p2) edge, v
-// from fv over (p0, p1)), decided as above; r = 1 / det
-__device__ inline bool tri_hit_fast(double dx, double dy, double ox, double oy, double ux,
-                                    double uy, double vx, double vy, double det, double r,
-                                    double umin, double uvmax, double margin) {
+struct QuadEdges {     // both triangles of a quad, hoisted for the pixel tests
+  double x0, y0, au1, au2, av1, av2, det_a, r_a;   // A = (p0, p1, p2)
+  double x3, y3, bu1, bu2, bv1, bv2, det_b, r_b;   // B = (p3, p2, p1)
+};
+
+// hit / no hit of one triangle from its numerators nu = _fu(...), nv =
+// _fv(...) (bit-identical to the reference's: the same float64 operations on
+// the same hoisted differences): decided by the reciprocal when every value
+// is clearly away from its limit, by the reference's divisions otherwise
+// (|u - nu/det| <= ~3 ulp(u): below the margin for |u| < 1e5, and beyond that
+// u is farther than its error from every limit — an absolute margin suffices)
+__device__ inline bool tri_decide(double nu, double nv, double det, double r, double umin,
+                                  double uvmax, double margin) {
   if (det == 0.0) return false;
-  const double nu = fu(dx, dy, ox, oy, ux, uy), nv = fv(dx, dy, ox, oy, vx, vy);
   const double u = nu * r, v = nv * r, s = u + v;
-  // |u - nu/det| <= ~3 ulp(u): below 1e-9 for |u| < 1e5, and beyond that u is
-  // farther than its error from every limit — an absolute margin suffices
   if (fabs(u - umin) > margin && fabs(v - umin) > margin && fabs(s - uvmax) > margin)
     return u >= umin && v >= umin && s <= uvmax;
   const double ue = nu / det, ve = nv / det;
   return ue >= umin && ve >= umin && ue + ve <= uvmax;
 }
 
-// ---- K5a: claim target pixels with the raster-order key of hitting quads -------
-// Phase 1, one quad per lane: lanes take consecutive quads of a window row, so
-// the right-hand corners (p1, p3) of a quad are the left-hand corners (p0, p2)
-// of the next lane's quad and come from it by a shuffle (only the last quad of
-// a row or of the wave loads them itself); the quad's clipped target-pixel
-// window and determinants are parked in LDS.
-// Phase 2, load-balanced: the wave's (quad, window pixel) tests are numbered by
-// a wave prefix sum of the window sizes and dealt round-robin to the 64 lanes
-// — every lane runs ceil(total / 64) tests instead of the wave running the
-// largest window of any lane (quads culled by the tile or degenerate cost
-// nothing), each test reading its quad from LDS.
-// Work list: chunk c belongs to the tile t with offs[t] <= c < offs[t+1] (the
-// offsets come from xrs_rectify_tiles on the device, or from the host); the
-// offsets are staged in LDS and searched per chunk.
-constexpr int kOffsLds = 2047;   // tiles whose offsets are copied to LDS (16 KB)
-constexpr int kQd = 12;          // doubles per staged quad: 8 corners, det_a/b, 1/det_a/b
+// rectify.py:556-573 for the target pixel centre (dx, dy): triangle A, then B
+__device__ inline bool quad_covers(const QuadEdges& e, double dx, double dy, double umin,
+                                   double uvmax, double margin) {
+  double ex = e.x0 - dx, ey = e.y0 - dy;
+  if (tri_decide(ex * e.au1 - ey * e.au2, ey * e.av1 - ex * e.av2, e.det_a, e.r_a, umin, uvmax,
+                 margin))
+    return true;
+  ex = e.x3 - dx;
+  ey = e.y3 - dy;
+  return tri_decide(ex * e.bu1 - ey * e.bu2, ey * e.bv1 - ex * e.bv2, e.det_b, e.r_b, umin,
+                    uvmax, margin);
+}
 
-struct ClaimLds {
-  double qd[kThreads / 64][kQd][64];
-  int32_t qi[kThreads / 64][4][64];   // imin, jmin, nw, key
-  int64_t qs[kThreads / 64][64];      // exclusive start of the quad's tests
+// the reference's test of one triangle at pixel centre (dx, dy)
+// (rectify.py:556-573): A = (p0; p2, p1), B = (p3; p1, p2)
+__device__ inline bool tri_exact(const Quad& q, bool tri_b, double dx, double dy, double umin,
+                                 double uvmax) {
+  double det, u, v;
+  if (!tri_b) {
+    det = fdet(q.x0, q.y0, q.x1, q.y1, q.x2, q.y2);
+    if (det != det || det == 0.0) return false;
+    u = fu(dx, dy, q.x0, q.y0, q.x2, q.y2) / det;
+    v = fv(dx, dy, q.x0, q.y0, q.x1, q.y1) / det;
+  } else {
+    det = fdet(q.x3, q.y3, q.x2, q.y2, q.x1, q.y1);
+    if (det != det || det == 0.0) return false;
+    u = fu(dx, dy, q.x3, q.y3, q.x1, q.y1) / det;
+    v = fv(dx, dy, q.x3, q.y3, q.x2, q.y2) / det;
+  }
+  return u >= umin && v >= umin && u + v <= uvmax;
+}
+
+__device__ inline double dpp_next_f64(double v) {   // lane i <- lane i + 1 (lane 63: 0)
+  const uint64_t b = __double_as_longlong(v);
+  const uint32_t lo = __builtin_amdgcn_mov_dpp((int)(uint32_t)b, 0x130, 0xF, 0xF, true);
+  const uint32_t hi = __builtin_amdgcn_mov_dpp((int)(uint32_t)(b >> 32), 0x130, 0xF, 0xF, true);
+  return __longlong_as_double((int64_t)(((uint64_t)hi << 32) | lo));
+}
+
+struct StripPoint {    // one source point of the strip
+  double x, y;
 };
+
+__device__ inline StripPoint strip_next(const StripPoint& p) {
+  return StripPoint{dpp_next_f64(p.x), dpp_next_f64(p.y)};
+}
+
+// floor of the extreme corner value q (min or max of the four corners' target
+// pixel units) when it is clearly away from an integer: then it equals the
+// min / max of the corners' exact np.floor((x - off) / scale) (the error of q
+// is a few ulps, far below the margin); false -> exact per-corner path
+__device__ inline bool floor_clear(double q, double margin, double& f) {
+  f = floor(q);
+  const double fr = q - f;
+  const double m = margin * (1.0 + fabs(q));
+  return fr > m && fr < 1.0 - m;
+}
+
+// the reference's int64 window bound of one axis from the four corners
+// (rectify.py:500-507): exact divisions, NaN / huge -> INT64_MIN
+__device__ inline void pix_range_exact(double c0, double c1, double c2, double c3, double off,
+                                       double scale, int64_t& lo, int64_t& hi) {
+  const int64_t p0 = f64_to_i64_x86(floor((c0 - off) / scale));
+  const int64_t p1 = f64_to_i64_x86(floor((c1 - off) / scale));
+  const int64_t p2 = f64_to_i64_x86(floor((c2 - off) / scale));
+  const int64_t p3 = f64_to_i64_x86(floor((c3 - off) / scale));
+  lo = min(min(p0, p1), min(p2, p3));
+  hi = max(max(p0, p1), max(p2, p3));
+}
+
+__device__ inline Quad load_quad32(const RectArgs& a, int32_t qj, int32_t qi) {
+  return load_quad(a, qj, qi);
+}
 
 __global__ void __launch_bounds__(kThreads)
 rectify_claim_kernel(RectArgs a) {
-  extern __shared__ __align__(16) unsigned char smem[];
-  ClaimLds& L = *reinterpret_cast<ClaimLds*>(smem);
-  int64_t* offs_s = reinterpret_cast<int64_t*>(smem + sizeof(ClaimLds));
+  __shared__ int64_t offs_s[kOffsLds + 1];
   const int lane = threadIdx.x & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const bool lds_offs = a.ntiles <= kOffsLds;
   if (lds_offs)
     for (int64_t t = threadIdx.x; t <= a.ntiles; t += kThreads) offs_s[t] = a.chunk_offs[t];
@@ -384,163 +455,215 @@ rectify_claim_kernel(RectArgs a) {
   const int64_t* offs = lds_offs ? offs_s : a.chunk_offs;
   const int64_t nchunks = offs[a.ntiles];
   const double umin = -a.uv_delta, uvmax = 1.0 + 2 * a.uv_delta;
-  for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+  const int64_t nwaves = (int64_t)gridDim.x * (kThreads / 64);
+  for (int64_t c = (int64_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6); c < nchunks;
+       c += nwaves) {
     int64_t lo = 0, hi = a.ntiles;   // last t with offs[t] <= c
     while (hi - lo > 1) {
       const int64_t m = (lo + hi) >> 1;
       if (offs[m] <= c) lo = m; else hi = m;
     }
+    lo = __builtin_amdgcn_readfirstlane((int32_t)lo);   // wave-uniform
     const TileInfo ti = a.tiles[lo];
-    const int32_t nq_i = ti.swin - 1;
-    const int64_t q = (c - offs[lo]) * kThreads + threadIdx.x;
-    const bool valid = ti.si0 >= 0 && nq_i > 0 && q < (int64_t)nq_i * (int64_t)(ti.shin - 1);
-    int32_t lj = 0, li = 0, qj = 0, qi = 0;
-    Quad Q{NAN, NAN, NAN, NAN, NAN, NAN, NAN, NAN};
-    int64_t pi0 = 0, pj0 = 0, pi2 = 0, pj2 = 0;
-    if (valid) {
-      lj = (int32_t)(q / nq_i);
-      li = (int32_t)(q - (int64_t)lj * nq_i);  // quad within the tile window
-      qj = ti.sj0 + lj;
-      qi = ti.si0 + li;                        // global quad corner p0
-      const int64_t r0 = (int64_t)qj * a.sy, r1 = (int64_t)(qj + 1) * a.sy;
-      Q.x0 = a.x[r0 + qi]; Q.y0 = a.y[r0 + qi];
-      Q.x2 = a.x[r1 + qi]; Q.y2 = a.y[r1 + qi];
-      pi0 = pix_fast(Q.x0, ti.x_off, a.x_scale, a.inv_x, a.margin);
-      pj0 = pix_fast(Q.y0, ti.y_off, a.y_scale, a.inv_y, a.margin);
-      pi2 = pix_fast(Q.x2, ti.x_off, a.x_scale, a.inv_x, a.margin);
-      pj2 = pix_fast(Q.y2, ti.y_off, a.y_scale, a.inv_y, a.margin);
-    }
-    // right-hand corners from the next lane (all lanes take part in shuffles)
-    Q.x1 = __shfl_down(Q.x0, 1, 64); Q.y1 = __shfl_down(Q.y0, 1, 64);
-    Q.x3 = __shfl_down(Q.x2, 1, 64); Q.y3 = __shfl_down(Q.y2, 1, 64);
-    int64_t pi1 = __shfl_down(pi0, 1, 64), pj1 = __shfl_down(pj0, 1, 64);
-    int64_t pi3 = __shfl_down(pi2, 1, 64), pj3 = __shfl_down(pj2, 1, 64);
-    int64_t cnt = 0;   // window pixels: up to a whole (untiled) target
-    int32_t imin32 = 0, jmin32 = 0, nw = 1;
-    double det_a = 0.0, det_b = 0.0;
-    if (valid) {
-      if (lane == 63 || li + 1 >= nq_i) {      // neighbour lane is not quad (lj, li+1)
-        const int64_t r0 = (int64_t)qj * a.sy, r1 = (int64_t)(qj + 1) * a.sy;
-        Q.x1 = a.x[r0 + qi + 1]; Q.y1 = a.y[r0 + qi + 1];
-        Q.x3 = a.x[r1 + qi + 1]; Q.y3 = a.y[r1 + qi + 1];
-        pi1 = pix_fast(Q.x1, ti.x_off, a.x_scale, a.inv_x, a.margin);
-        pj1 = pix_fast(Q.y1, ti.y_off, a.y_scale, a.inv_y, a.margin);
-        pi3 = pix_fast(Q.x3, ti.x_off, a.x_scale, a.inv_x, a.margin);
-        pj3 = pix_fast(Q.y3, ti.y_off, a.y_scale, a.inv_y, a.margin);
+    const int32_t nq_i = ti.swin - 1, nq_j = ti.shin - 1;
+    const int32_t ncx = (nq_i + kStripW - 1) / kStripW;
+    const int32_t cc = (int32_t)(c - offs[lo]);
+    const int32_t cy = cc / ncx, cx = cc - cy * ncx;
+    const int32_t pcol = cx * kStripW + lane;          // point column in the window
+    const bool has_pt = pcol <= nq_i;
+    const bool has_q = lane < kStripW && pcol < nq_i;  // quad (row, pcol) exists
+    const int32_t qi = ti.si0 + pcol;
+    const int32_t r_end = min(cy * kStripH + kStripH, nq_j);
+    auto load_pt = [&](int32_t qj) {
+      StripPoint p{NAN, NAN};
+      if (has_pt) {
+        const int64_t o = (int64_t)qj * a.sy + qi;
+        p.x = a.x[o];
+        p.y = a.y[o];
       }
-      int64_t imin = min(min(pi0, pi1), min(pi2, pi3)), imax = max(max(pi0, pi1), max(pi2, pi3));
-      int64_t jmin = min(min(pj0, pj1), min(pj2, pj3)), jmax = max(max(pj0, pj1), max(pj2, pj3));
-      if (!(imax < 0 || jmax < 0 || imin >= ti.tw || jmin >= ti.th)) {
-        imin = max(imin, (int64_t)0); jmin = max(jmin, (int64_t)0);
-        imax = min(imax, (int64_t)ti.tw - 1); jmax = min(jmax, (int64_t)ti.th - 1);
-        quad_dets(Q, det_a, det_b);
-        if (!(det_a == 0.0 && det_b == 0.0)) {
-          imin32 = (int32_t)imin;
-          jmin32 = (int32_t)jmin;
-          nw = (int32_t)(imax - imin + 1);
-          cnt = (int64_t)nw * (jmax - jmin + 1);
+      return p;
+    };
+    // target pixel units by the reciprocal (window floors)
+    auto qx = [&](double x) { return (x - ti.x_off) * a.inv_x; };
+    auto qy = [&](double y) { return (y - ti.y_off) * a.inv_y; };
+    StripPoint t0 = load_pt(ti.sj0 + cy * kStripH);
+    StripPoint t1 = strip_next(t0);
+    for (int32_t r = cy * kStripH; r < r_end; ++r) {
+      const int32_t qj = ti.sj0 + r;                    // global quad row (corner p0)
+      const StripPoint b0 = load_pt(qj + 1);
+      const StripPoint b1 = strip_next(b0);
+      // corners p0 = t0, p1 = t1, p2 = b0, p3 = b1
+      int64_t cnt = 0;
+      int32_t imin = 0, jmin = 0, nw = 0, nh = 0;
+      QuadEdges e{};
+      if (has_q) {
+        double fx0, fx1, fy0, fy1;
+        // floor is monotone and the reciprocal's error tiny: the extremes of the
+        // coordinates give the extreme pixel units
+        const double qx0 = qx(fmin(fmin(t0.x, t1.x), fmin(b0.x, b1.x)));
+        const double qx1 = qx(fmax(fmax(t0.x, t1.x), fmax(b0.x, b1.x)));
+        const double qy0 = qy(a.y_scale > 0 ? fmin(fmin(t0.y, t1.y), fmin(b0.y, b1.y))
+                                            : fmax(fmax(t0.y, t1.y), fmax(b0.y, b1.y)));
+        const double qy1 = qy(a.y_scale > 0 ? fmax(fmax(t0.y, t1.y), fmax(b0.y, b1.y))
+                                            : fmin(fmin(t0.y, t1.y), fmin(b0.y, b1.y)));
+        const double fin = t0.x + t1.x + b0.x + b1.x + t0.y + t1.y + b0.y + b1.y;
+        int64_t i0, i1, j0, j1;
+        if (fin - fin == 0.0 && fmax(fabs(qx0), fabs(qx1)) < 0x1p40 &&
+            fmax(fabs(qy0), fabs(qy1)) < 0x1p40 && floor_clear(qx0, a.margin, fx0) &&
+            floor_clear(qx1, a.margin, fx1) && floor_clear(qy0, a.margin, fy0) &&
+            floor_clear(qy1, a.margin, fy1)) {
+          i0 = (int64_t)fx0; i1 = (int64_t)fx1; j0 = (int64_t)fy0; j1 = (int64_t)fy1;
+        } else {
+          pix_range_exact(t0.x, t1.x, b0.x, b1.x, ti.x_off, a.x_scale, i0, i1);
+          pix_range_exact(t0.y, t1.y, b0.y, b1.y, ti.y_off, a.y_scale, j0, j1);
+        }
+        if (!(i1 < 0 || j1 < 0 || i0 >= ti.tw || j0 >= ti.th)) {
+          i0 = max(i0, (int64_t)0); j0 = max(j0, (int64_t)0);
+          i1 = min(i1, (int64_t)ti.tw - 1); j1 = min(j1, (int64_t)ti.th - 1);
+          // edge factors = the differences inside the reference's _fdet / _fu / _fv
+          const double au1 = t0.y - b0.y, au2 = t0.x - b0.x;   // _fu(p, p0, p2)
+          const double av1 = t0.x - t1.x, av2 = t0.y - t1.y;   // _fv(p, p0, p1)
+          const double bu1 = b1.y - t1.y, bu2 = b1.x - t1.x;   // _fu(p, p3, p1)
+          const double bv1 = b1.x - b0.x, bv2 = b1.y - b0.y;   // _fv(p, p3, p2)
+          double det_a = av1 * au1 - au2 * av2;   // _fdet(p0, p1, p2)
+          double det_b = bv1 * bu1 - bu2 * bv2;   // _fdet(p3, p2, p1)
+          if (det_a != det_a) det_a = 0.0;
+          if (det_b != det_b) det_b = 0.0;
+          if (!(det_a == 0.0 && det_b == 0.0)) {
+            imin = (int32_t)i0; jmin = (int32_t)j0;
+            nw = (int32_t)(i1 - i0 + 1);
+            nh = (int32_t)(j1 - j0 + 1);
+            cnt = (int64_t)nw * nh;
+            e.x0 = t0.x; e.y0 = t0.y; e.au1 = au1; e.au2 = au2; e.av1 = av1; e.av2 = av2;
+            e.det_a = det_a; e.r_a = det_a != 0.0 ? 1.0 / det_a : 0.0;
+            e.x3 = b1.x; e.y3 = b1.y; e.bu1 = bu1; e.bu2 = bu2; e.bv1 = bv1; e.bv2 = bv2;
+            e.det_b = det_b; e.r_b = det_b != 0.0 ? 1.0 / det_b : 0.0;
+          }
         }
       }
+      const uint32_t key = (uint32_t)qj * (uint32_t)a.w + (uint32_t)qi;
+      // small windows: every lane walks its own
+      {
+        const int32_t n = cnt <= kLaneWindow ? (int32_t)cnt : 0;
+        int32_t di = imin, dj = jmin;
+        uint32_t* row = a.keys + (int64_t)(ti.r0 + dj) * a.dst_w + ti.c0;
+        for (int32_t k = 0; k < n; ++k) {
+          const double dy = ti.y_off + ((double)dj + 0.5) * a.y_scale;
+          const double dx = ti.x_off + ((double)di + 0.5) * a.x_scale;
+          if (quad_covers(e, dx, dy, umin, uvmax, a.uv_margin)) atomicMin(row + di, key);
+          if (++di == imin + nw) {
+            di = imin;
+            ++dj;
+            row += a.dst_w;
+          }
+        }
+      }
+      // large windows: one quad at a time, walked by the whole wave (exact test)
+      uint64_t big = __ballot(cnt > kLaneWindow);
+      while (big) {
+        const int o = __builtin_ctzll(big);
+        big &= big - 1;
+        const int32_t oqi = __builtin_amdgcn_readlane(qi, o);
+        const Quad Q = load_quad32(a, qj, oqi);
+        const int32_t wi0 = __builtin_amdgcn_readlane(imin, o);
+        const int32_t wj0 = __builtin_amdgcn_readlane(jmin, o);
+        const int32_t wnw = __builtin_amdgcn_readlane(nw, o);
+        const uint32_t wkey = __builtin_amdgcn_readlane(key, o);
+        const int64_t wcnt =
+            ((int64_t)__builtin_amdgcn_readlane((uint32_t)(cnt >> 32), o) << 32) |
+            __builtin_amdgcn_readlane((uint32_t)cnt, o);
+        // test k = lane + 64 s sits at (row k / wnw, column k % wnw), stepped exactly
+        const int32_t step_r = 64 / wnw, step_c = 64 % wnw;
+        int64_t dj = lane / wnw;
+        int32_t di = lane % wnw;
+        for (int64_t k = lane; k < wcnt; k += 64) {
+          const double dy = ti.y_off + ((double)(wj0 + dj) + 0.5) * a.y_scale;
+          const double dx = ti.x_off + ((double)(wi0 + di) + 0.5) * a.x_scale;
+          if (tri_exact(Q, false, dx, dy, umin, uvmax) || tri_exact(Q, true, dx, dy, umin, uvmax))
+            atomicMin(a.keys + (int64_t)(ti.r0 + wj0 + dj) * a.dst_w + ti.c0 + wi0 + di, wkey);
+          dj += step_r;
+          di += step_c;
+          if (di >= wnw) { di -= wnw; ++dj; }
+        }
+      }
+      t0 = b0;
+      t1 = b1;
     }
-    // wave-exclusive prefix sum of the window sizes (int64: a quad with a NaN
-    // corner spans its whole tile, rectify.py:500-526, and a tile may be a
-    // whole untiled target)
-    int64_t incl = cnt;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int64_t v = __shfl_up(incl, o, 64);
-      if (lane >= o) incl += v;
-    }
-    const int64_t total = __shfl(incl, 63, 64);
-    if (total == 0) continue;
-    double* qd = &L.qd[wv][0][0];
-    int32_t* qs = &L.qi[wv][0][0];
-    int64_t* qst = &L.qs[wv][0];
-    qd[0 * 64 + lane] = Q.x0; qd[1 * 64 + lane] = Q.y0;
-    qd[2 * 64 + lane] = Q.x1; qd[3 * 64 + lane] = Q.y1;
-    qd[4 * 64 + lane] = Q.x2; qd[5 * 64 + lane] = Q.y2;
-    qd[6 * 64 + lane] = Q.x3; qd[7 * 64 + lane] = Q.y3;
-    qd[8 * 64 + lane] = det_a; qd[9 * 64 + lane] = det_b;
-    qd[10 * 64 + lane] = det_a != 0.0 ? 1.0 / det_a : 0.0;
-    qd[11 * 64 + lane] = det_b != 0.0 ? 1.0 / det_b : 0.0;
-    qs[0 * 64 + lane] = imin32; qs[1 * 64 + lane] = jmin32; qs[2 * 64 + lane] = nw;
-    qs[3 * 64 + lane] = (int32_t)((int64_t)qj * a.w + qi);
-    qst[lane] = incl - cnt;   // exclusive start
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    for (int64_t k = lane; k < total; k += 64) {
-      int32_t o = 0;                   // owner: last lane with start <= k
-#pragma unroll
-      for (int step = 32; step > 0; step >>= 1)
-        if (qst[o + step] <= k) o += step;
-      // (row, column) of test `local` in the owner's window of w_ columns: the
-      // float quotient is within +-1 of local / w_ (window rows < 2^22, checked
-      // by xrs_rectify_ij), the integer remainder corrects it exactly
-      const int64_t local = k - qst[o];
-      const int32_t w_ = qs[2 * 64 + o];
-      int64_t q_ = (int64_t)((float)local / (float)w_);
-      int64_t r_ = local - q_ * w_;
-      if (r_ < 0) { --q_; r_ += w_; }
-      else if (r_ >= w_) { ++q_; r_ -= w_; }
-      const int32_t di = qs[0 * 64 + o] + (int32_t)r_;
-      const int32_t dj = qs[1 * 64 + o] + (int32_t)q_;
-      const double x0 = qd[0 * 64 + o], y0 = qd[1 * 64 + o], x1 = qd[2 * 64 + o],
-                   y1 = qd[3 * 64 + o], x2 = qd[4 * 64 + o], y2 = qd[5 * 64 + o],
-                   x3 = qd[6 * 64 + o], y3 = qd[7 * 64 + o];
-      const double dy = ti.y_off + ((double)dj + 0.5) * a.y_scale;
-      const double dx = ti.x_off + ((double)di + 0.5) * a.x_scale;
-      const bool hit =
-          tri_hit_fast(dx, dy, x0, y0, x2, y2, x1, y1, qd[8 * 64 + o], qd[10 * 64 + o], umin,
-                       uvmax, a.margin) ||
-          tri_hit_fast(dx, dy, x3, y3, x1, y1, x2, y2, qd[9 * 64 + o], qd[11 * 64 + o], umin,
-                       uvmax, a.margin);
-      if (hit)
-        atomicMin(a.keys + (int64_t)(ti.r0 + dj) * a.dst_w + ti.c0 + di,
-                  (uint32_t)qs[3 * 64 + o]);
-    }
-    __builtin_amdgcn_wave_barrier();   // the next chunk rewrites this wave's LDS slots
   }
 }
 
 // ---- K5b: resolve the winning quad of every target pixel ------------------------
+// Work item = one tile x kResolveRows target rows (tile fields are block-
+// uniform: no per-pixel tile search or 64-bit division); each thread takes one
+// column of the item's rows and issues the key loads of all its rows, then the
+// winning quads' corner loads of all its rows, before any arithmetic — three
+// dependent memory round trips per kResolveRows pixels instead of per pixel.
+constexpr int kResolveRows = 4;
+
 __global__ void __launch_bounds__(kThreads)
-rectify_resolve_kernel(RectArgs a, int64_t ntiles_x) {
+rectify_resolve_kernel(RectArgs a) {
   const int64_t n = a.dst_h * a.dst_w;
-  for (int64_t p = (int64_t)blockIdx.x * kThreads + threadIdx.x; p < n;
-       p += (int64_t)gridDim.x * kThreads) {
-    const uint32_t key = a.keys[p];
-    double oi = NAN, oj = NAN;
-    if (key != 0xFFFFFFFFu) {
-      const int64_t r = p / a.dst_w, c = p - r * a.dst_w;
-      const TileInfo& ti0 = a.tiles[0];
-      const int64_t t = (r / ti0.th) * ntiles_x + c / ti0.tw;  // tile 0 has the full tile size
-      const TileInfo ti = a.tiles[t];
-      const int64_t qj = key / a.w, qi = key - qj * a.w;
-      const Quad Q = load_quad(a, qj, qi);
-      double det_a, det_b;
-      quad_dets(Q, det_a, det_b);
-      const int64_t dj = r - ti.r0, di = c - ti.c0;
-      const double dy = ti.y_off + ((double)dj + 0.5) * a.y_scale;
-      const double dx = ti.x_off + ((double)di + 0.5) * a.x_scale;
-      double cu, cv;
-      const int tri = quad_hit(a, Q, dx, dy, det_a, det_b, cu, cv);
-      if (tri) {
-        const int64_t li = qi - ti.si0, lj = qj - ti.sj0;   // tile-local quad indices
-        double src_i, src_j;
-        if (tri == 1) {
-          src_i = (double)li + cu;                           // src_i0 + clamp(u)
-          src_j = (double)lj + cv;
-        } else {
-          src_i = (double)(li + 1) - cu;                     // src_i1 - clamp(u)
-          src_j = (double)(lj + 1) - cv;
+  // tile 0 has the full tile height (edge tiles are shorter)
+  const int64_t bands = (a.tiles[0].th + kResolveRows - 1) / kResolveRows;
+  const int64_t nitems = a.ntiles * bands;
+  const double inv_w = 1.0 / (double)a.w;
+  for (int64_t it = blockIdx.x; it < nitems; it += gridDim.x) {
+    const int64_t t = it / bands;
+    const int32_t rb = (int32_t)(it - t * bands) * kResolveRows;
+    const TileInfo ti = a.tiles[t];
+    if (rb >= ti.th) continue;
+    const int32_t nr = min(kResolveRows, ti.th - rb);
+    for (int32_t di = threadIdx.x; di < ti.tw; di += kThreads) {
+      const int64_t p0 = (int64_t)(ti.r0 + rb) * a.dst_w + ti.c0 + di;
+      uint32_t key[kResolveRows];
+#pragma unroll
+      for (int r = 0; r < kResolveRows; ++r)
+        key[r] = r < nr ? a.keys[p0 + r * a.dst_w] : 0xFFFFFFFFu;
+      Quad Q[kResolveRows];
+      int64_t qj[kResolveRows], qi[kResolveRows];
+#pragma unroll
+      for (int r = 0; r < kResolveRows; ++r) {
+        if (key[r] != 0xFFFFFFFFu) {
+          // key / w through the reciprocal, corrected to the exact quotient
+          int64_t j = (int64_t)((double)key[r] * inv_w);
+          int64_t i = (int64_t)key[r] - j * a.w;
+          if (i < 0) { --j; i += a.w; } else if (i >= a.w) { ++j; i -= a.w; }
+          qj[r] = j;
+          qi[r] = i;
+          Q[r] = load_quad(a, j, i);
         }
-        oi = (double)ti.si0 + src_i;                         // src_i_min + src_i
-        oj = (double)ti.sj0 + src_j;
+      }
+#pragma unroll
+      for (int r = 0; r < kResolveRows; ++r) {
+        if (r >= nr) break;
+        double oi = NAN, oj = NAN;
+        if (key[r] != 0xFFFFFFFFu) {
+          double det_a, det_b;
+          quad_dets(Q[r], det_a, det_b);
+          const int32_t dj = rb + r;
+          const double dy = ti.y_off + ((double)dj + 0.5) * a.y_scale;
+          const double dx = ti.x_off + ((double)di + 0.5) * a.x_scale;
+          double cu, cv;
+          const int tri = quad_hit(a, Q[r], dx, dy, det_a, det_b, cu, cv);
+          if (tri) {
+            const int64_t li = qi[r] - ti.si0, lj = qj[r] - ti.sj0;   // tile-local quad
+            double src_i, src_j;
+            if (tri == 1) {
+              src_i = (double)li + cu;                                 // src_i0 + clamp(u)
+              src_j = (double)lj + cv;
+            } else {
+              src_i = (double)(li + 1) - cu;                           // src_i1 - clamp(u)
+              src_j = (double)(lj + 1) - cv;
+            }
+            oi = (double)ti.si0 + src_i;                               // src_i_min + src_i
+            oj = (double)ti.sj0 + src_j;
+          }
+        }
+        const int64_t p = p0 + r * a.dst_w;
+        a.ij[p] = oi;
+        a.ij[n + p] = oj;
       }
     }
-    a.ij[p] = oi;
-    a.ij[n + p] = oj;
   }
 }
 
@@ -599,7 +722,7 @@ rectify_var_kernel(const double* __restrict__ ij, int64_t dst_h, int64_t dst_w,
 // ij_border and clipped, source window = [i_min, min(i_max + 1, w)), target
 // offsets dst_x_min + c0 * res (python float arithmetic, no contraction).
 // One block: records in parallel, then an exclusive scan of the per-tile
-// 256-quad chunk counts.
+// strip counts (kStripH x kStripW quads).
 __global__ void __launch_bounds__(kThreads)
 rectify_tiles_kernel(const int32_t* __restrict__ acc, int64_t ntx, int64_t nty, int64_t tw,
                      int64_t th, int64_t dst_w, int64_t dst_h, int64_t src_w, int64_t src_h,
@@ -638,9 +761,9 @@ rectify_tiles_kernel(const int32_t* __restrict__ acc, int64_t ntx, int64_t nty, 
       ti.x_off = x_min + (double)ti.c0 * x_res;
       ti.y_off = j_up ? y_min + (double)ti.r0 * y_res : y_max - (double)ti.r0 * y_res;
       tiles[t] = ti;
-      const int64_t nq = none ? 0 : max((int64_t)ti.swin - 1, (int64_t)0) *
-                                        max((int64_t)ti.shin - 1, (int64_t)0);
-      nch = (nq + kThreads - 1) / kThreads;
+      const int64_t nqi = none ? 0 : max((int64_t)ti.swin - 1, (int64_t)0);
+      const int64_t nqj = none ? 0 : max((int64_t)ti.shin - 1, (int64_t)0);
+      nch = ((nqi + kStripW - 1) / kStripW) * ((nqj + kStripH - 1) / kStripH);
     }
     // inclusive scan of nch over the block (Hillis-Steele in LDS)
     part[threadIdx.x] = nch;
@@ -716,7 +839,7 @@ extern "C" int xrs_rectify_ij(const double* x, const double* y, int64_t h, int64
   using namespace xrs;
   if (!x || !y || !tiles || !keys || !ij || h < 2 || w < 2 || sy < w || ntiles < 1 ||
       dst_h < 1 || dst_w < 1 || h * w >= (int64_t)UINT32_MAX || !chunk_offsets || max_chunks < 0 ||
-      dst_h >= (1 << 22) || dst_w > INT32_MAX) {
+      dst_h > INT32_MAX || dst_w > INT32_MAX) {
     xrs_set_error("xrs_rectify_ij: invalid argument");
     return XRS_ERR_ARG;
   }
@@ -729,20 +852,20 @@ extern "C" int xrs_rectify_ij(const double* x, const double* y, int64_t h, int64
   a.inv_x = 1.0 / x_scale; a.inv_y = 1.0 / y_scale;
   // tests: xrs_testing_set(XRS_TESTING_RECTIFY_EXACT, 1) takes the exact
   // divisions for every decision
-  a.margin = xrs_testing_value(XRS_TESTING_RECTIFY_EXACT) != 0 ? INFINITY : kMargin;
+  const bool exact = xrs_testing_value(XRS_TESTING_RECTIFY_EXACT) != 0;
+  a.margin = exact ? INFINITY : kMargin;
+  a.uv_margin = exact ? INFINITY : kUvMargin;
   hipStream_t st = static_cast<hipStream_t>(stream);
   XRS_HIP_CHECK(hipMemsetAsync(keys, 0xFF, (size_t)(dst_h * dst_w) * sizeof(uint32_t), st));
   {
-    // one chunk per block when the caller knows the chunk count, else 16 blocks per CU
-    const int nb = max_chunks > 0 ? grid_blocks(max_chunks, 1, 1 << 24)
-                                  : grid_blocks(256 * 16, 1, 1 << 24);
-    const size_t lds = sizeof(ClaimLds) +
-                       (ntiles <= kOffsLds ? (size_t)(ntiles + 1) * sizeof(int64_t) : 0);
-    hipLaunchKernelGGL(rectify_claim_kernel, dim3(nb), dim3(kThreads), lds, st, a);
+    // one strip per wave when the caller knows the strip count, else 8 blocks per CU
+    const int nb = max_chunks > 0 ? grid_blocks(max_chunks, kThreads / 64, 1 << 24)
+                                  : grid_blocks(256 * 8, 1, 1 << 24);
+    hipLaunchKernelGGL(rectify_claim_kernel, dim3(nb), dim3(kThreads), 0, st, a);
     XRS_HIP_CHECK(hipGetLastError());
   }
-  const int nb2 = grid_blocks(dst_h * dst_w, kThreads, 256 * 8);
-  hipLaunchKernelGGL(rectify_resolve_kernel, dim3(nb2), dim3(kThreads), 0, st, a, ntiles_x);
+  const int nb2 = grid_blocks(256 * 32, 1, 1 << 24);
+  hipLaunchKernelGGL(rectify_resolve_kernel, dim3(nb2), dim3(kThreads), 0, st, a);
   XRS_HIP_CHECK(hipGetLastError());
   return XRS_OK;
 }

@@ -195,6 +195,18 @@ def rectify_tiles_device(x_image, y_image, target_xy_bboxes, xy_border: float, i
     return tiles, offs
 
 
+# K5a work list: strips of STRIP_H quad rows x STRIP_W quads per tile window
+# (xrs_rectify.hip kStripW / kStripH, one wave per strip)
+STRIP_W, STRIP_H = 63, 16
+
+
+def strip_counts(swin, shin):
+    """Number of K5a strips over tile windows of swin x shin source pixels."""
+    nqi = np.maximum(np.asarray(swin, np.int64) - 1, 0)
+    nqj = np.maximum(np.asarray(shin, np.int64) - 1, 0)
+    return (nqi + STRIP_W - 1) // STRIP_W * ((nqj + STRIP_H - 1) // STRIP_H)
+
+
 def rectify_ij(x_image, y_image, tiles: np.ndarray, ntiles_x: int, dst_h: int, dst_w: int,
                x_scale: float, y_scale: float, uv_delta: float, device=None, stream=None):
     """K5 — per target pixel the fractional source (i, j) (rectify.py:373-576).
@@ -209,10 +221,7 @@ def rectify_ij(x_image, y_image, tiles: np.ndarray, ntiles_x: int, dst_h: int, d
     h, w = x.shape
     if isinstance(tiles, np.ndarray):   # host tiles: offsets computed here
         tiles = np.ascontiguousarray(tiles, dtype=TILE_INFO_DTYPE)
-        nq = np.where(tiles["si0"] >= 0,
-                      np.maximum(tiles["swin"].astype(np.int64) - 1, 0)
-                      * np.maximum(tiles["shin"].astype(np.int64) - 1, 0), 0)
-        nch = (nq + 255) // 256
+        nch = np.where(tiles["si0"] >= 0, strip_counts(tiles["swin"], tiles["shin"]), 0)
         offs_h = np.concatenate([[0], np.cumsum(nch)]).astype(np.int64)
         ntiles, max_chunks = len(tiles), int(offs_h[-1])
         t_dev = torch().from_numpy(tiles.view(np.uint8).copy()).to(device)
