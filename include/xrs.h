@@ -307,6 +307,42 @@ int xrs_rectify_var(const double* ij, int64_t dst_h, int64_t dst_w, const void* 
 #define XRS_TESTING_NUM_KNOBS 8
 int64_t xrs_testing_set(int knob, int64_t value);
 
+/* ---- coordinate transformation (reproject.py:472-496, rectify.py:182-231) --
+ * xrs_transform — the reference's per-point pyproj transformation for CRS
+ *   pairs that are not separable, as a pipeline of up to XRS_MAX_PROJ_STEPS
+ *   PROJ operations (source -> geographic -> target: [inverse], [forward] or
+ *   [inverse, forward]; degrees for geographic,
+ *   metres for projected CRSs, always_xy order).  Each step restates PROJ's
+ *   operation as xcube_resampling_amd/projections.py does (results agree with
+ *   that numpy restatement to a few ulps: device libm).
+ *   grid != 0: x (w,), y (h,) are a grid's axes, point (r, c) = (x[c], y[r]);
+ *   grid == 0: x, y are (h, w) row-major images.  out_x, out_y: (h, w).
+ *   steps: HOST array of nsteps records (copied at the call).
+ */
+#define XRS_MAX_PROJ_STEPS 4
+#define XRS_PROJ_WEBMERC_FWD 1   /* degrees -> EPSG:3857 metres (merc_s, webmerc) */
+#define XRS_PROJ_WEBMERC_INV 2
+#define XRS_PROJ_TMERC_FWD 3     /* tmerc, poder_engsager (UTM: k0 0.9996, ...)   */
+#define XRS_PROJ_TMERC_INV 4
+#define XRS_PROJ_LAEA_FWD 5      /* laea, ellipsoidal                              */
+#define XRS_PROJ_LAEA_INV 6
+
+typedef struct XrsProjStep {
+  int32_t kind;      /* XRS_PROJ_* */
+  int32_t mode;      /* laea aspect: 0 north pole, 1 south pole, 2 equatorial, 3 oblique */
+  double a, ra;      /* semi-major axis, 1 / a */
+  double x0, y0;     /* false easting / northing (metres) */
+  double lam0, phi0; /* central meridian / latitude of origin (radians) */
+  double e, es, one_es;
+  double c[24];      /* tmerc: cgb[6], cbg[6], utg[6], gtu[6] */
+  double Qn, Zb;     /* tmerc */
+  double qp, mmf, apa[3], rq, dd, xmf, ymf, sinb1, cosb1;   /* laea */
+} XrsProjStep;
+
+int xrs_transform(const double* x, const double* y, int64_t w, int64_t h, int grid,
+                  const XrsProjStep* steps, int nsteps, double* out_x, double* out_y,
+                  void* stream);
+
 #ifdef __cplusplus
 }
 #endif

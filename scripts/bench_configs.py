@@ -142,6 +142,63 @@ def config2(args):
           8 * size * size + 4 * s_read, "gather_separable_kernel<float,double,1>", cpu)
 
 
+# ------------------------------------------------------ config 2u
+def config2u(args):
+    """Reproject bilinear 8192^2 f32 UTM 32N (EPSG:32632) -> LAEA Europe
+    (EPSG:3035), 2048^2 tiles: a non-separable pair, per-pixel transform on
+    the device (xrs_transform) + K1 on the 2-D coordinate tables."""
+    import torch
+
+    import xcube_resampling_amd as xrs
+    from xcube_resampling_amd import kernels
+
+    size, res = 8192, 30.0
+    sgm = xrs.GridMapping.regular((size, size), (400000.0, 5400000.0), res, "EPSG:32632",
+                                  tile_size=2048)
+    tgm = xrs.GridMapping.regular((size, size), (4180000.0, 2870000.0), res, "EPSG:3035",
+                                  tile_size=2048)
+    tr = xrs.Transformer.from_crs(tgm.crs, sgm.crs, always_xy=True)
+    plan = xrs.plan_reproject(sgm, tgm, tr)
+    assert plan.coord_mode == 1
+    g = torch.Generator(device="cuda")
+    g.manual_seed(20250905)
+    src = torch.rand((1, size, size), generator=g, device="cuda", dtype=torch.float32)
+    out = torch.empty((1, size, size), device="cuda", dtype=torch.float64)
+    flags = kernels.ErrorFlags(src.device)
+
+    def end_to_end():   # coordinate tables rebuilt every step, then K1
+        plan._device_cache.clear()
+        kernels.reproject(src, plan, "bilinear", float("nan"), out=out, flags=flags)
+
+    gx = torch.from_numpy(plan.grid_x).cuda()
+    gy = torch.from_numpy(plan.grid_y).cuda()
+    t_ms, _ = _timed(lambda: kernels.transform(tr, gx, gy, True), args.steps, args.warmup)
+    plan.device_tables(src.device)
+    k_ms, _ = _timed(lambda: kernels.reproject(src, plan, "bilinear", float("nan"), out=out,
+                                               flags=flags), args.steps, args.warmup)
+    e_ms, wall = _timed(end_to_end, max(3, args.steps // 4), 1)
+    flags.raise_if_set("config 2u")
+    covered = int(torch.isfinite(out).sum().item())
+    # CPU: the numpy restatement of the per-pixel transformation of 2048^2 tiles
+    # (the reference's _transform_gridpoints, its dominant per-tile cost)
+    xx, yy = np.meshgrid(plan.grid_x[:2048], plan.grid_y[:2048])
+    cpu_v, px, dt = _cpu_loop(lambda: (tr.transform(xx, yy), xx.size)[1], args.cpu_seconds, 0)
+    # algorithmic bytes of the end-to-end step: tables written + read (32 B/px),
+    # f64 out, f32 source reads (<= the source once)
+    alg = 16 * size * size + 16 * size * size + 8 * size * size + 4 * size * size
+    _line("2u", "reproject bilinear 8192x8192 f32 UTM 32N (EPSG:32632) -> LAEA Europe "
+                "(EPSG:3035) 30 m, 2048^2 tiles, f64 out; per-pixel transform on the device "
+                "(xrs_transform: tmerc inverse + laea forward) then K1 on 2-D tables, end to end",
+          size * size, e_ms, wall, alg,
+          f"transform_kernel<true> {t_ms:.3f} ms + gather K1 (2-D tables) {k_ms:.3f} ms",
+          dict(value=round(cpu_v, 2), unit="Mpixels/s", cores=1, kind="port",
+               sample=f"numpy restatement of the per-pixel UTM -> LAEA transform "
+                      f"(projections.py) over {px // xx.size} 2048^2 tiles in {dt:.1f} s, "
+                      "one thread (the transform alone; the block gather is not included)"),
+          {"transform_ms": round(t_ms, 4), "k1_ms": round(k_ms, 4), "covered_px": covered,
+           "transform_gpts_s": round(size * size / (t_ms / 1e3) / 1e9, 2)})
+
+
 # ------------------------------------------------------------------ config 3
 def config3(args):
     """Coarsen mean 4x4: 16384^2 f32 -> 4096^2 (bilinear upscale at scale 1 + nanmean)."""
@@ -291,7 +348,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     args = ap.parse_args()
     for c in args.configs.split(","):
-        {"1": config1, "2": config2, "3": config3, "4": config4}[c.strip()](args)
+        {"1": config1, "2": config2, "2u": config2u, "3": config3,
+         "4": config4}[c.strip()](args)
 
 
 if __name__ == "__main__":

@@ -1,0 +1,124 @@
+"""GPU tests of xrs_transform, the device coordinate transformation of the
+non-separable CRS pairs (reproject.py:472-496 per target pixel,
+rectify.py:182-231 per source pixel).
+
+Bar: the device pipeline restates the numpy restatement of PROJ
+(xcube_resampling_amd/projections.py + crs.py) operation by operation; the
+device libm rounds some transcendentals differently in the last bit, so the
+two agree to a few ulps (tolerances below, in units of the coordinate), with
+non-finite results (outside a projection's domain, NaN input) in exactly the
+same places.  Downstream, a reprojection through the device tables equals the
+one through host tables wherever no source index lands within those ulps of a
+pixel boundary (checked on an 8192-pixel-wide UTM -> LAEA grid), and the
+reference's own PROJ-pinned goldens still pass (tests/test_crs_gpu.py)."""
+
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+# |device - numpy| bounds: metres for projected targets, degrees for geographic
+# (far from a transverse Mercator's central meridian the series amplify the
+# last-bit differences of sin / atan2 / asinh to ~1e-13 relative)
+ATOL = {"m": 1e-7, "deg": 1e-12}
+RTOL = 1e-12
+
+
+def _grid(crs, n=257):
+    """Axes of a grid over the CRS's area of use (plus points outside it)."""
+    if crs in ("EPSG:4326",):
+        return np.linspace(-179.5, 179.5, n), np.linspace(-89.5, 89.5, n)
+    if crs == "EPSG:3857":
+        return np.linspace(-2.0e7, 2.0e7, n), np.linspace(-2.0e7, 2.0e7, n)
+    if crs == "EPSG:3035":
+        return np.linspace(1.0e6, 7.5e6, n), np.linspace(0.5e6, 6.0e6, n)
+    # UTM: easting 160 km - 840 km (and a strip outside), northing 0 - 9300 km
+    return np.linspace(-2.0e6, 3.0e6, n), np.linspace(0.0, 9.3e6, n)
+
+
+@pytest.mark.parametrize("src,dst", [
+    ("EPSG:32632", "EPSG:3035"),
+    ("EPSG:3035", "EPSG:32632"),
+    ("EPSG:4326", "EPSG:32633"),
+    ("EPSG:32733", "EPSG:4326"),
+    ("EPSG:3035", "EPSG:4326"),
+    ("EPSG:4326", "EPSG:3035"),
+    ("EPSG:3857", "EPSG:32610"),
+    ("EPSG:4326", "EPSG:3857"),
+    ("EPSG:3857", "EPSG:4326"),
+])
+def test_device_transform_matches_numpy_restatement(src, dst):
+    import xcube_resampling_amd as xrs
+    from xcube_resampling_amd import kernels
+
+    tr = xrs.Transformer.from_crs(src, dst, always_xy=True)
+    gx, gy = _grid(src)
+    xx, yy = np.meshgrid(gx, gy)
+    ex, ey = tr.transform(xx, yy)
+    dx, dy = (t.cpu().numpy() for t in kernels.transform(tr, gx, gy, True))
+    for got, exp in ((dx, ex), (dy, ey)):
+        fin = np.isfinite(exp)
+        np.testing.assert_array_equal(np.isfinite(got), fin)
+        np.testing.assert_array_equal(np.isnan(got), np.isnan(exp))
+        unit = "deg" if xrs.CRS.from_user_input(dst).is_geographic else "m"
+        assert fin.sum() > 0.2 * fin.size
+        np.testing.assert_allclose(got[fin], exp[fin], rtol=RTOL, atol=ATOL[unit])
+    # image mode == grid mode
+    ix, iy = (t.cpu().numpy() for t in kernels.transform(tr, xx, yy, False))
+    np.testing.assert_array_equal(ix, dx)
+    np.testing.assert_array_equal(iy, dy)
+
+
+def test_device_transform_nan_inputs():
+    import xcube_resampling_amd as xrs
+    from xcube_resampling_amd import kernels
+
+    tr = xrs.Transformer.from_crs("EPSG:3035", "EPSG:32632", always_xy=True)
+    x = np.array([[4.3e6, np.nan, 4.0e6], [np.inf, 4.1e6, 4.2e6]])
+    y = np.array([[3.3e6, 3.0e6, np.nan], [3.1e6, -np.inf, 3.2e6]])
+    ex, ey = tr.transform(x, y)
+    dx, dy = (t.cpu().numpy() for t in kernels.transform(tr, x, y, False))
+    for got, exp in ((dx, ex), (dy, ey)):
+        np.testing.assert_array_equal(np.isnan(got), np.isnan(exp))
+        np.testing.assert_array_equal(np.isinf(got), np.isinf(exp))
+
+
+def test_reproject_utm_to_laea_device_tables_match_host_tables():
+    """An 8192-pixel-wide LAEA target over a UTM 32N source: the plan's 2-D
+    coordinate tables made on the device vs the numpy restatement, and the
+    bilinear / nearest reprojection through either."""
+    import dataclasses
+
+    import torch
+
+    import xcube_resampling_amd as xrs
+    from xcube_resampling_amd import kernels
+
+    n = 2048
+    sgm = xrs.GridMapping.regular((n, n), (400000.0, 5500000.0), 100.0, "EPSG:32632",
+                                  tile_size=512)
+    tgm = xrs.GridMapping.regular((8192, 256), (4200000.0, 2980000.0), 25.0, "EPSG:3035",
+                                  tile_size=(2048, 256))
+    tr = xrs.Transformer.from_crs(tgm.crs, sgm.crs, always_xy=True)
+    plan = xrs.plan_reproject(sgm, tgm, tr)
+    assert plan.coord_mode == 1 and plan.src_x is None
+    hx, hy = plan.host_coords()
+    tabs = plan.device_tables("cuda:0")
+    dx, dy = tabs["src_x"].cpu().numpy(), tabs["src_y"].cpu().numpy()
+    np.testing.assert_allclose(dx, hx, rtol=0, atol=ATOL["m"])
+    np.testing.assert_allclose(dy, hy, rtol=0, atol=ATOL["m"])
+    host_plan = dataclasses.replace(plan, src_x=hx, src_y=hy, _device_cache={})
+    src = torch.rand((1, n, n), generator=torch.Generator().manual_seed(3)).cuda()
+    # nearest: equal except where a source index lies within those ulps of a
+    # pixel boundary; bilinear (float64 weights, continuous): equal to ~1e-9
+    a = kernels.reproject(src, plan, "nearest", np.nan).cpu().numpy()
+    b = kernels.reproject(src, host_plan, "nearest", np.nan).cpu().numpy()
+    same = (a == b) | (np.isnan(a) & np.isnan(b))
+    assert same.mean() > 0.9999, same.mean()
+    assert np.isfinite(a).mean() > 0.5
+    a = kernels.reproject(src, plan, "bilinear", np.nan).cpu().numpy()
+    b = kernels.reproject(src, host_plan, "bilinear", np.nan).cpu().numpy()
+    np.testing.assert_array_equal(np.isnan(a), np.isnan(b))
+    np.testing.assert_allclose(a, b, rtol=0, atol=2e-9)   # weights differ by ~1e-9 (1e-7 m / 100 m)

@@ -102,7 +102,26 @@ _SIGNATURES = {
     "xrs_testing_set": (_c_i64, [_c_int, _c_i64]),
     "xrs_rectify_var": (_c_int, [_c_ptr, _c_i64, _c_i64, _c_ptr, _c_int, _c_i64, _c_i64, _c_i64,
                                  _c_i64, _c_i64, _c_ptr, _c_i64, _c_int, _c_dbl, _c_ptr]),
+    "xrs_transform": (_c_int, [_c_ptr, _c_ptr, _c_i64, _c_i64, _c_int, _c_ptr, _c_int, _c_ptr,
+                               _c_ptr, _c_ptr]),
 }
+
+
+class ProjStep(ctypes.Structure):
+    """XrsProjStep (include/xrs.h): one PROJ operation of an xrs_transform pipeline."""
+
+    _fields_ = [("kind", ctypes.c_int32), ("mode", ctypes.c_int32),
+                ("a", _c_dbl), ("ra", _c_dbl), ("x0", _c_dbl), ("y0", _c_dbl),
+                ("lam0", _c_dbl), ("phi0", _c_dbl), ("e", _c_dbl), ("es", _c_dbl),
+                ("one_es", _c_dbl), ("c", _c_dbl * 24), ("Qn", _c_dbl), ("Zb", _c_dbl),
+                ("qp", _c_dbl), ("mmf", _c_dbl), ("apa", _c_dbl * 3), ("rq", _c_dbl),
+                ("dd", _c_dbl), ("xmf", _c_dbl), ("ymf", _c_dbl), ("sinb1", _c_dbl),
+                ("cosb1", _c_dbl)]
+
+
+PROJ_KINDS = {"webmerc_fwd": 1, "webmerc_inv": 2, "tmerc_fwd": 3, "tmerc_inv": 4,
+              "laea_fwd": 5, "laea_inv": 6}
+MAX_PROJ_STEPS = 4
 
 TESTING_KNOBS = {"reproject_band": 1, "reproject_blocks_per_cu": 2, "affine_generic": 3,
                  "rectify_exact": 4}

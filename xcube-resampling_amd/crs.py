@@ -413,6 +413,42 @@ def _projection(crs: CRS):
     return hit
 
 
+def _proj_step(crs: CRS, inverse: bool):
+    """The xrs_transform record (include/xrs.h XrsProjStep) of crs._projection
+    forward / inverse: the same constants the numpy restatement uses."""
+    from ._native import PROJ_KINDS, ProjStep
+
+    st = ProjStep()
+    if crs.kind == "webmerc":
+        st.kind = PROJ_KINDS["webmerc_inv" if inverse else "webmerc_fwd"]
+        st.a, st.ra = _WGS84_A, 1.0 / _WGS84_A
+        return st
+    from .projections import LambertAzimuthalEqualArea, TransverseMercator
+    ell_name, lon_0, lat_0, k0, x_0, y_0 = crs.params
+    ell = _ellipsoid(ell_name)
+    st.a, st.ra, st.x0, st.y0 = ell.a, 1.0 / ell.a, x_0, y_0
+    st.lam0, st.phi0 = lon_0 * _DEG_TO_RAD, lat_0 * _DEG_TO_RAD
+    st.e, st.es, st.one_es = ell.e, ell.es, ell.one_es
+    if crs.kind == "tmerc":
+        proj = TransverseMercator(ell, k0, st.phi0)
+        st.kind = PROJ_KINDS["tmerc_inv" if inverse else "tmerc_fwd"]
+        for k, v in enumerate(list(proj.cgb) + list(proj.cbg) + list(proj.utg) + list(proj.gtu)):
+            st.c[k] = v
+        st.Qn, st.Zb = proj.Qn, proj.Zb
+    else:
+        proj = LambertAzimuthalEqualArea(ell, st.phi0)
+        st.kind = PROJ_KINDS["laea_inv" if inverse else "laea_fwd"]
+        st.mode = {"npole": 0, "spole": 1, "equit": 2, "obliq": 3}[proj.mode]
+        st.qp, st.mmf = proj.qp, proj.mmf
+        for k in range(3):
+            st.apa[k] = proj.apa[k]
+        st.dd = proj.dd
+        for name in ("rq", "xmf", "ymf", "sinb1", "cosb1"):
+            if hasattr(proj, name):
+                setattr(st, name, getattr(proj, name))
+    return st
+
+
 class Transformer:
     """Subset of ``pyproj.Transformer`` used by the reference (always_xy).
 
@@ -426,12 +462,16 @@ class Transformer:
         if same:
             self._fn = None
             self._separable = True
+            self._step_crs = []
             return
         steps = []
+        self._step_crs = []   # (crs, inverse) per step: the device pipeline (xrs_transform)
         if not crs_from.is_geographic:
             steps.append(_projection(crs_from)[1])
+            self._step_crs.append((crs_from, True))
         if not crs_to.is_geographic:
             steps.append(_projection(crs_to)[0])
+            self._step_crs.append((crs_to, False))
 
         def fn(xx, yy, steps=tuple(steps)):
             for step in steps:
@@ -458,6 +498,16 @@ class Transformer:
         """x' depends only on x and y' only on y (identity, geographic <-> web
         Mercator); other pairs need 2-D coordinate tables."""
         return self._separable
+
+    def device_steps(self):
+        """The pipeline as a ctypes array of XrsProjStep records for
+        xrs_transform (kernels.transform)."""
+        from ._native import ProjStep
+
+        arr = (ProjStep * max(1, len(self._step_crs)))()
+        for k, (crs, inverse) in enumerate(self._step_crs):
+            arr[k] = _proj_step(crs, inverse)
+        return arr, len(self._step_crs)
 
     def transform(self, xx, yy):
         xx = np.asarray(xx, dtype=np.float64)

@@ -10,6 +10,8 @@ rectify.py is built on them.
 
 from __future__ import annotations
 
+import ctypes
+
 import numpy as np
 
 from . import _native
@@ -193,6 +195,30 @@ def rectify_tiles_device(x_image, y_image, target_xy_bboxes, xy_border: float, i
         stream_handle(device, stream))
     _native.check(rc, "xrs_rectify_tiles")
     return tiles, offs
+
+
+def transform(transformer, x, y, grid: bool, device=None, stream=None):
+    """xrs_transform: the transformer's pipeline on the device
+    (reproject.py:472-496 / rectify.py:182-231 per-point pyproj calls).
+
+    grid=True: x (W,), y (H,) axes of a regular grid -> (H, W) images of the
+    transformed pixel centres; grid=False: x, y (H, W) images.  Returns two
+    float64 device tensors (H, W)."""
+    device = require_device(device if device is not None else getattr(x, "device", None))
+    xd = to_device(x, device, np.float64)
+    yd = to_device(y, device, np.float64)
+    if grid:
+        h, w = yd.numel(), xd.numel()
+    else:
+        h, w = xd.shape
+    ox = torch().empty((h, w), dtype=torch().float64, device=device)
+    oy = torch().empty((h, w), dtype=torch().float64, device=device)
+    steps, nsteps = transformer.device_steps()
+    rc = _native.lib().xrs_transform(ptr(xd), ptr(yd), w, h, 1 if grid else 0,
+                                     ctypes.cast(steps, ctypes.c_void_p), nsteps, ptr(ox),
+                                     ptr(oy), stream_handle(device, stream))
+    _native.check(rc, "xrs_transform")
+    return ox, oy
 
 
 # K5a work list: strips of STRIP_H quad rows x STRIP_W quads per tile window

@@ -55,8 +55,8 @@ class ReprojectPlan:
     x_res: float
     y_res: float
     coord_mode: int              # 0: separable tables, 1: 2-D tables
-    src_x: np.ndarray            # (W',) or (H', W') float64, target pixel x in source CRS
-    src_y: np.ndarray            # (H',) or (H', W') float64
+    src_x: np.ndarray | None     # (W',) or (H', W') float64, target pixel x in source CRS
+    src_y: np.ndarray | None     # (H',) or (H', W') float64 (None: 2-D tables made on device)
     tile_x0: np.ndarray          # (ntiles,) float32, window x origin (reproject.py:427-453)
     tile_y0: np.ndarray          # (ntiles,) float32
     tile_win: np.ndarray         # (ntiles, 2) int64, window (i0, j0) in unpadded source indices
@@ -64,6 +64,11 @@ class ReprojectPlan:
     win_height: int
     scr_ij_bboxes: np.ndarray    # (4, nty, ntx) int32, as returned by the reference (padded)
     pad_width: tuple
+    # 2-D plans without host tables: the target grid's pixel-centre axes and the
+    # target -> source transformer, evaluated per pixel on the device
+    grid_x: np.ndarray | None = None
+    grid_y: np.ndarray | None = None
+    transformer: Transformer | None = None
     _device_cache: dict = field(default_factory=dict, repr=False)
 
     @property
@@ -74,15 +79,30 @@ class ReprojectPlan:
         key = str(device)
         tabs = self._device_cache.get(key)
         if tabs is None:
+            if self.src_x is None:   # target pixel centres -> source CRS on the device
+                from . import kernels
+                sx, sy = kernels.transform(self.transformer, self.grid_x, self.grid_y, True,
+                                           device)
+            else:
+                sx = to_device(np.ascontiguousarray(self.src_x, np.float64), device)
+                sy = to_device(np.ascontiguousarray(self.src_y, np.float64), device)
             tabs = dict(
-                src_x=to_device(np.ascontiguousarray(self.src_x, np.float64), device),
-                src_y=to_device(np.ascontiguousarray(self.src_y, np.float64), device),
+                src_x=sx,
+                src_y=sy,
                 tile_x0=to_device(self.tile_x0.astype(np.float32), device),
                 tile_y0=to_device(self.tile_y0.astype(np.float32), device),
                 tile_win=to_device(np.ascontiguousarray(self.tile_win, np.int64), device),
             )
             self._device_cache[key] = tabs
         return tabs
+
+    def host_coords(self) -> tuple[np.ndarray, np.ndarray]:
+        """The coordinate tables on the host (2-D plans: the numpy
+        restatement of the transformation, reproject.py:472-496)."""
+        if self.src_x is not None:
+            return self.src_x, self.src_y
+        xx, yy = np.meshgrid(self.grid_x, self.grid_y)
+        return self.transformer.transform(xx, yy)
 
     def workspace(self, device, nbytes: int):
         """Device scratch for the axis tables (reused across calls; stream-ordered)."""
@@ -228,20 +248,23 @@ def plan_reproject(source_gm: GridMapping, target_gm: GridMapping,
         coord_mode = 0
         src_x = transformer.transform_x(tx)
         src_y = transformer.transform_y(ty)
-    else:
+    else:   # evaluated per target pixel on the device (xrs_transform)
         coord_mode = 1
-        xx, yy = np.meshgrid(tx, ty)
-        src_x, src_y = transformer.transform(xx, yy)
+        src_x = src_y = None
 
     return ReprojectPlan(
         src_width=source_gm.width, src_height=source_gm.height,
         dst_width=target_gm.width, dst_height=target_gm.height,
         tile_width=target_gm.tile_width, tile_height=target_gm.tile_height,
         x_res=source_gm.x_res, y_res=source_gm.y_res, coord_mode=coord_mode,
-        src_x=np.asarray(src_x, np.float64), src_y=np.asarray(src_y, np.float64),
+        src_x=None if src_x is None else np.asarray(src_x, np.float64),
+        src_y=None if src_y is None else np.asarray(src_y, np.float64),
         tile_x0=tile_x0, tile_y0=tile_y0, tile_win=tile_win,
         win_width=int(i_diff_max), win_height=int(j_diff_max),
         scr_ij_bboxes=scr_ij_bboxes, pad_width=pad_width,
+        grid_x=None if coord_mode == 0 else np.asarray(tx, np.float64),
+        grid_y=None if coord_mode == 0 else np.asarray(ty, np.float64),
+        transformer=None if coord_mode == 0 else transformer,
     )
 
 
