@@ -278,11 +278,13 @@ int xrs_rectify_tiles(const int32_t* acc, int64_t ntiles_x, int64_t ntiles_y, in
 /* -------------------------------------------------------------------------
  * xrs_rectify_var — replaces _compute_var_image_block / _sequential /
  * _for_dest_line (rectify.py:605-734): sample a (n, src_h, src_w) variable
- * at the fractional source positions ij (2, dst_h, dst_w); nearest (u > 0.5
+ * at the fractional source positions ij (2, dst_h, dst_w): i plane at ij, j
+ * plane at ij + ij_sn (a row band of a larger ij image: ij points at the
+ * band's first row, ij_sn = the whole image's plane size); nearest (u > 0.5
  * rounds up), triangular or bilinear in float64, stored in the variable
  * dtype; NaN positions -> fill.  dst: (n, dst_h, dst_w), slice stride dst_sn.
  * ------------------------------------------------------------------------- */
-int xrs_rectify_var(const double* ij, int64_t dst_h, int64_t dst_w, const void* src,
+int xrs_rectify_var(const double* ij, int64_t ij_sn, int64_t dst_h, int64_t dst_w, const void* src,
                     int src_dtype, int64_t n, int64_t src_h, int64_t src_w, int64_t src_sn,
                     int64_t src_sy, void* dst, int64_t dst_sn, int interp, double fill,
                     void* stream);

@@ -3,6 +3,7 @@ each band needs before its kernel may run."""
 
 from __future__ import annotations
 
+import numpy as np
 import pytest
 
 from helpers import load_golden, reproject_golden_inputs
@@ -46,3 +47,39 @@ def test_band_source_rows_cover_every_read(rows):
     assert his == sorted(his) and his[-1] <= plan.src_height
     for (r0, r1), (_, j1) in zip(bands, src_rows):
         assert plan.source_rows_for(r0, r1)[1] <= j1
+
+
+def test_source_rows_copies_only_missing_runs():
+    """_SourceRows copies each needed row once, in contiguous runs, whatever
+    the order of the requests."""
+    from xcube_resampling_amd import streaming
+
+    calls = []
+    orig = streaming._copy
+    streaming._copy = lambda dst, src, nbytes, stream: calls.append(nbytes)
+    try:
+        class _Dev:   # stand-in device buffer: only data_ptr() is used
+            def __getitem__(self, idx):
+                return type("R", (), {"data_ptr": lambda self: 0})()
+
+        src = np.zeros((2, 100, 8), np.float32)
+        rows = streaming._SourceRows(src, _Dev(), None)
+        rows.need(40, 60)
+        rows.need(10, 50)        # rows 10..39 missing -> one run
+        rows.need(55, 70)        # rows 60..69
+        rows.need(-5, 5)         # clipped to 0..4
+        rows.need(30, 20)        # empty
+    finally:
+        streaming._copy = orig
+    row = 8 * 4
+    assert calls == [20 * row] * 2 + [30 * row] * 2 + [10 * row] * 2 + [5 * row] * 2
+    assert rows.resident[0:5].all() and rows.resident[10:70].all()
+    assert not rows.resident[5:10].any() and not rows.resident[70:].any()
+
+
+def test_band_rows_multiple_of_unit():
+    from xcube_resampling_amd.streaming import _band_rows
+
+    assert _band_rows(1000, 1 << 20, 8) % 8 == 0
+    assert _band_rows(10, 1, 8) == 16     # whole (rounded-up) height in one band
+    assert _band_rows(5000, 64 << 20, 7) == 7

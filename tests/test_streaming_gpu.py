@@ -141,3 +141,74 @@ def test_streamed_from_read_only_memmap(tmp_path):
     src = np.load(tmp_path / "src.npy", mmap_mode="r")
     out = streaming.reproject_host(src, _plan(g), "bilinear", g["fill"].item(), band_rows=7)
     assert_bitwise_equal(out, g["out_bilinear"], "memmap source")
+
+
+# ---- affine / rectify band pipelines (streaming.affine_host / rectify_host) ------
+AFFINE_CASES = [
+    # (matrix, out (h, w), out chunks (h, w), order, agg)
+    (((0.9216, 0.0, 102.4), (0.0, 0.9216, 51.2)), (700, 650), (128, 160), 0, "first"),
+    (((0.5, 0.0, 3.25), (0.0, 0.5, 7.5)), (900, 800), (256, 200), 1, "first"),
+    (((4.0, 0.0, 0.0), (0.0, 4.0, 0.0)), (200, 220), (64, 100), 1, "mean"),
+    (((3.0, 0.0, 1.0), (0.0, 3.0, 2.0)), (180, 200), (60, 75), 1, "max"),
+]
+
+
+@pytest.mark.parametrize("band_chunks", [1, 2, None])
+@pytest.mark.parametrize("case", range(len(AFFINE_CASES)))
+def test_affine_streamed_matches_resident(case, band_chunks):
+    """Bands of whole output chunk rows, each reading only its chunks' input
+    slices (the device source is poisoned with NaN bytes beforehand, so a read
+    outside a band's rows would show) == the resident launch, bit for bit."""
+    import torch
+
+    import xcube_resampling_amd.affine as A
+    from xcube_resampling_amd import kernels, streaming
+
+    m, out_shape, chunks, order, agg = AFFINE_CASES[case]
+    rng = np.random.default_rng(case)
+    src = rng.random((2, 800, 900), dtype=np.float32)
+    src.ravel()[rng.choice(src.size, 300, replace=False)] = np.nan
+    plan = A.plan_affine(src.shape, src.dtype, m, (2,) + out_shape, (1,) + chunks, order, agg,
+                         False, np.nan)
+    ref = kernels.affine(torch.from_numpy(src).cuda(), plan).cpu().numpy()
+    out = streaming.affine_host(src, plan, band_chunks=band_chunks, poison=True)
+    assert out is not None
+    assert_bitwise_equal(out, ref, f"affine case {case} band_chunks={band_chunks}")
+
+
+def _swath_ij(h, w, reverse):
+    import torch
+
+    import xcube_resampling_amd as xrs
+    from xcube_resampling_amd import rectify as R
+
+    ii, jj = np.meshgrid(np.arange(w), np.arange(h))
+    rng = np.random.default_rng(11)
+    sign = 1 if reverse else -1
+    lat = 60 + sign * 0.0027 * jj - 0.0004 * ii + rng.normal(0, 1e-4, (h, w))
+    lon = 5 + 0.0045 * ii + 0.0009 * jj + rng.normal(0, 1e-4, (h, w))
+    sgm = xrs.GridMapping.from_coords(xrs.DataArray(lon, ("y", "x"), name="lon"),
+                                      xrs.DataArray(lat, ("y", "x"), name="lat"), "EPSG:4326")
+    tgm = sgm.to_regular(tile_size=128)
+    return R._compute_target_source_ij(sgm, tgm, 1e-3)
+
+
+@pytest.mark.parametrize("reverse", [False, True])
+@pytest.mark.parametrize("band_rows", [1, 37, None])
+def test_rectify_streamed_matches_resident(band_rows, reverse):
+    """K6 in target row bands, each reading only the source rows its
+    positions reach (bounded per row from ij; a swath whose rows run against
+    the target's exercises out-of-order row needs) == the resident K6."""
+    import torch
+
+    from xcube_resampling_amd import kernels, streaming
+
+    h, w = 600, 500
+    ij = _swath_ij(h, w, reverse)
+    rng = np.random.default_rng(3)
+    src = rng.random((2, h, w), dtype=np.float32)
+    for interp in ("nearest", "bilinear", "triangular"):
+        ref = kernels.rectify_var(ij, torch.from_numpy(src).cuda(), interp, np.nan).cpu().numpy()
+        out = streaming.rectify_host(src, ij, interp, np.nan, band_rows=band_rows, poison=True)
+        assert_bitwise_equal(out, ref, f"rectify {interp} band_rows={band_rows}")
+    assert np.isfinite(ref).mean() > 0.4

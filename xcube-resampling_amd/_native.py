@@ -100,8 +100,8 @@ _SIGNATURES = {
                                    _c_i64, _c_i64, _c_i64, _c_dbl, _c_dbl, _c_dbl, _c_dbl,
                                    _c_dbl, _c_int, _c_ptr, _c_ptr, _c_ptr]),
     "xrs_testing_set": (_c_i64, [_c_int, _c_i64]),
-    "xrs_rectify_var": (_c_int, [_c_ptr, _c_i64, _c_i64, _c_ptr, _c_int, _c_i64, _c_i64, _c_i64,
-                                 _c_i64, _c_i64, _c_ptr, _c_i64, _c_int, _c_dbl, _c_ptr]),
+    "xrs_rectify_var": (_c_int, [_c_ptr, _c_i64, _c_i64, _c_i64, _c_ptr, _c_int, _c_i64, _c_i64,
+                                 _c_i64, _c_i64, _c_i64, _c_ptr, _c_i64, _c_int, _c_dbl, _c_ptr]),
     "xrs_transform": (_c_int, [_c_ptr, _c_ptr, _c_i64, _c_i64, _c_int, _c_ptr, _c_int, _c_ptr,
                                _c_ptr, _c_ptr]),
 }

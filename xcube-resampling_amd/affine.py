@@ -21,6 +21,8 @@ import numpy as np
 from . import _native, kernels
 from .dataset import DataArray, Dataset
 from .device import is_device_array, require_device, to_device
+from . import streaming
+from .options import get_options
 from .streaming import device_to_host, host_to_device
 from .gridmapping import GridMapping
 from .utils import (
@@ -287,6 +289,16 @@ def _resample_array(data, dims, chunks, affine_matrix, output_shape, output_chun
     if len(data.shape) > 3:
         raise NotImplementedError("the engine resamples 2-D and 3-D variables")
     device = require_device()
+    if isinstance(data, np.ndarray) and data.ndim in (2, 3) and \
+            data.nbytes >= get_options()["host_streaming_min_bytes"] and \
+            not (recover_nan and interp > 0 and np.issubdtype(data.dtype, np.floating)):
+        # numpy in, numpy out (affine.py:227-228): band pipeline, no NaN test needed
+        arr = data.reshape((1,) + data.shape) if data.ndim == 2 else data
+        plan = plan_affine(arr.shape, arr.dtype, affine_matrix, output_shape, output_chunks,
+                           interp, agg, False, fill_value)
+        res = streaming.affine_host(arr, plan, device)
+        if res is not None:
+            return res[0] if data.ndim == 2 else res
     src = host_to_device(data, device)
     expanded = src.dim() == 2
     if expanded:

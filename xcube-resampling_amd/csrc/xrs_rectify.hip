@@ -670,7 +670,7 @@ rectify_resolve_kernel(RectArgs a) {
 // ---- K6: per-variable sampling (rectify.py:663-734) ------------------------------
 template <typename T, int INTERP>
 __global__ void __launch_bounds__(kThreads)
-rectify_var_kernel(const double* __restrict__ ij, int64_t dst_h, int64_t dst_w,
+rectify_var_kernel(const double* __restrict__ ij, int64_t ij_sn, int64_t dst_h, int64_t dst_w,
                    const T* __restrict__ src, int64_t n, int64_t src_h, int64_t src_w,
                    int64_t src_sn, int64_t src_sy, T* __restrict__ dst, int64_t dst_sn,
                    double fill) {
@@ -678,7 +678,7 @@ rectify_var_kernel(const double* __restrict__ ij, int64_t dst_h, int64_t dst_w,
   const T tfill = Conv<T>::from_f64(fill);
   for (int64_t p = (int64_t)blockIdx.x * kThreads + threadIdx.x; p < np;
        p += (int64_t)gridDim.x * kThreads) {
-    const double fi = ij[p], fj = ij[np + p];
+    const double fi = ij[p], fj = ij[ij_sn + p];
     if (fi != fi || fj != fj) {
       for (int64_t s = 0; s < n; ++s) dst[s * dst_sn + p] = tfill;
       continue;
@@ -870,7 +870,8 @@ extern "C" int xrs_rectify_ij(const double* x, const double* y, int64_t h, int64
   return XRS_OK;
 }
 
-extern "C" int xrs_rectify_var(const double* ij, int64_t dst_h, int64_t dst_w, const void* src,
+extern "C" int xrs_rectify_var(const double* ij, int64_t ij_sn, int64_t dst_h, int64_t dst_w,
+                               const void* src,
                                int src_dtype, int64_t n, int64_t src_h, int64_t src_w,
                                int64_t src_sn, int64_t src_sy, void* dst, int64_t dst_sn,
                                int interp, double fill, void* stream) {
@@ -881,7 +882,7 @@ extern "C" int xrs_rectify_var(const double* ij, int64_t dst_h, int64_t dst_w, c
     return XRS_ERR_NOTIMPL;
   }
   if (!ij || !src || !dst || dst_h < 1 || dst_w < 1 || n < 1 || src_h < 1 || src_w < 1 ||
-      src_sy < src_w || dst_sn < dst_h * dst_w) {
+      src_sy < src_w || dst_sn < dst_h * dst_w || ij_sn < dst_h * dst_w) {
     xrs_set_error("xrs_rectify_var: invalid argument");
     return XRS_ERR_ARG;
   }
@@ -893,13 +894,13 @@ extern "C" int xrs_rectify_var(const double* ij, int64_t dst_h, int64_t dst_w, c
     T* d = static_cast<T*>(dst);
     if (interp == XRS_INTERP_NEAREST)
       hipLaunchKernelGGL((rectify_var_kernel<T, XRS_INTERP_NEAREST>), dim3(nb), dim3(kThreads),
-                         0, st, ij, dst_h, dst_w, s, n, src_h, src_w, src_sn, src_sy, d, dst_sn, fill);
+                         0, st, ij, ij_sn, dst_h, dst_w, s, n, src_h, src_w, src_sn, src_sy, d, dst_sn, fill);
     else if (interp == XRS_INTERP_TRIANGULAR)
       hipLaunchKernelGGL((rectify_var_kernel<T, XRS_INTERP_TRIANGULAR>), dim3(nb), dim3(kThreads),
-                         0, st, ij, dst_h, dst_w, s, n, src_h, src_w, src_sn, src_sy, d, dst_sn, fill);
+                         0, st, ij, ij_sn, dst_h, dst_w, s, n, src_h, src_w, src_sn, src_sy, d, dst_sn, fill);
     else
       hipLaunchKernelGGL((rectify_var_kernel<T, XRS_INTERP_BILINEAR>), dim3(nb), dim3(kThreads),
-                         0, st, ij, dst_h, dst_w, s, n, src_h, src_w, src_sn, src_sy, d, dst_sn, fill);
+                         0, st, ij, ij_sn, dst_h, dst_w, s, n, src_h, src_w, src_sn, src_sy, d, dst_sn, fill);
     XRS_HIP_CHECK(hipGetLastError());
     return XRS_OK;
   });

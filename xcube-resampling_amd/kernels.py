@@ -265,9 +265,11 @@ def rectify_ij(x_image, y_image, tiles: np.ndarray, ntiles_x: int, dst_h: int, d
     return ij
 
 
-def rectify_var(ij, src, interp: str, fill, stream=None):
+def rectify_var(ij, src, interp: str, fill, stream=None, rows=None, out=None):
     """K6 — sample one variable (n, H, W) at the fractional source positions
-    `ij` (2, H', W') (rectify.py:605-734).  Returns (n, H', W') in src dtype."""
+    `ij` (2, H', W') (rectify.py:605-734).  Returns (n, H', W') in src dtype,
+    or with ``rows=(r0, r1)`` the target rows [r0, r1) into ``out`` (n, r1-r0,
+    W') (default: a new tensor)."""
     device = src.device
     code = _native.INTERP_CODES.get(interp)
     if code is None:
@@ -276,10 +278,19 @@ def rectify_var(ij, src, interp: str, fill, stream=None):
             f"'triangular', was '{interp}'.")
     n, h, w = src.shape
     _, dh, dw = ij.shape
-    out = torch().empty((n, dh, dw), dtype=src.dtype, device=device)
-    rc = _native.lib().xrs_rectify_var(ptr(ij), dh, dw, ptr(src), _native.DTYPE_CODES[_np_dtype(src)],
-                                       n, h, w, src.stride(0), src.stride(1), ptr(out), dh * dw,
-                                       code, float(fill), stream_handle(device, stream))
+    r0, r1 = rows if rows is not None else (0, dh)
+    if not 0 <= r0 < r1 <= dh:
+        raise ValueError(f"rows {rows} outside the target's {dh} rows")
+    if out is None:
+        out = torch().empty((n, r1 - r0, dw), dtype=src.dtype, device=device)
+    elif tuple(out.shape) != (n, r1 - r0, dw) or out.dtype != src.dtype or \
+            out.stride()[1:] != (dw, 1):
+        raise ValueError("out must be (n, rows, W') in the source dtype, rows contiguous")
+    ij = ij.contiguous()
+    rc = _native.lib().xrs_rectify_var(
+        ptr(ij) + r0 * dw * 8, dh * dw, r1 - r0, dw, ptr(src),
+        _native.DTYPE_CODES[_np_dtype(src)], n, h, w, src.stride(0), src.stride(1), ptr(out),
+        out.stride(0), code, float(fill), stream_handle(device, stream))
     _native.check(rc, "xrs_rectify_var")
     return out
 
@@ -294,6 +305,12 @@ def _workspace(device, nbytes: int):
         ws = torch().empty(max(nbytes, 1), dtype=torch().uint8, device=device)
         _WORKSPACES[key] = ws
     return ws
+
+
+def reserve_affine_workspace(device, ih: int, iw: int) -> None:
+    """Allocate the K2/K3 workspace for an (ih, iw) intermediate up front (a
+    band pipeline must not reallocate it while launches are in flight)."""
+    _workspace(device, _native.lib().xrs_affine_workspace_size(ih, iw))
 
 
 def any_nan(src, stream=None) -> bool:

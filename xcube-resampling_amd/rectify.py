@@ -29,6 +29,8 @@ from .constants import SCALE_LIMIT, UV_DELTA
 from .crs import Transformer
 from .dataset import DataArray, Dataset
 from .device import is_device_array, require_device, to_device
+from . import streaming
+from .options import get_options
 from .streaming import device_to_host, host_to_device
 from .gridmapping import GridMapping
 from .gridmapping.helpers import chunk_sizes
@@ -88,9 +90,18 @@ def rectify_dataset(source_ds, target_gm: GridMapping | None = None,
 
 def _transform_coords(source_ds: Dataset, source_gm: GridMapping,
                       target_gm: GridMapping) -> Dataset:
-    """rectify.py:182-231 — 2-D source coordinates into the target CRS."""
+    """rectify.py:182-231 — 2-D source coordinates into the target CRS, per
+    point on the device (xrs_transform); the host keeps a copy for the
+    GridMapping analysis of the transformed coordinates."""
     tr = Transformer.from_crs(source_gm.crs, target_gm.crs, always_xy=True)
-    xx, yy = tr.transform(source_gm.x_coords.values, source_gm.y_coords.values)
+    sx, sy = source_gm.x_coords.values, source_gm.y_coords.values
+    if tr.is_identity:
+        xx, yy = tr.transform(sx, sy)
+    else:
+        shape = np.shape(sx)
+        xd, yd = kernels.transform(tr, np.reshape(sx, (1, -1)), np.reshape(sy, (1, -1)), False,
+                                   require_device())
+        xx, yy = device_to_host(xd).reshape(shape), device_to_host(yd).reshape(shape)
     source_ds = source_ds.drop_vars(source_gm.xy_var_names)
     yx_dims = (source_gm.xy_dim_names[1], source_gm.xy_dim_names[0])
     names = ("lon", "lat") if target_gm.crs.is_geographic else ("transformed_x", "transformed_y")
@@ -197,15 +208,21 @@ def _rectify_data_array(data_array: DataArray, var_name, target_gm: GridMapping,
     fill_value = _get_fill_value(fill_values, var_name, data_array)
     interp_method = _get_interp_method_str(interp_methods, var_name, data_array)
     device = require_device()
-    on_device = is_device_array(data_array.data)
-    src = host_to_device(data_array.data, device)
-    expanded = src.dim() == 2
-    if expanded:
-        src = src.unsqueeze(0)
-    out = kernels.rectify_var(target_source_ij, src, interp_method, fill_value)
-    if expanded:
-        out = out[0]
+    data = data_array.data
+    if isinstance(data, np.ndarray) and data.ndim in (2, 3) and \
+            data.nbytes >= get_options()["host_streaming_min_bytes"]:
+        # numpy in, numpy out (rectify.py:297-298): band pipeline
+        arr = data.reshape((1,) + data.shape) if data.ndim == 2 else data
+        result = streaming.rectify_host(arr, target_source_ij, interp_method, fill_value, device)
+    else:
+        src = host_to_device(data, device)
+        if src.dim() == 2:
+            src = src.unsqueeze(0)
+        out = kernels.rectify_var(target_source_ij, src, interp_method, fill_value)
+        result = out if is_device_array(data) else device_to_host(out)
+    if data.ndim == 2:
+        result = result[0]
         dims = (target_gm.xy_dim_names[1], target_gm.xy_dim_names[0])
     else:
         dims = (data_array.dims[0], target_gm.xy_dim_names[1], target_gm.xy_dim_names[0])
-    return DataArray(out if on_device else device_to_host(out), dims, data_array.attrs)
+    return DataArray(result, dims, data_array.attrs)

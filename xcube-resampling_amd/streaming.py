@@ -195,3 +195,172 @@ def reproject_host(src: np.ndarray, plan, interp: str, fill: float, out_dtype=No
             s_out.synchronize()
     flags.raise_if_set("reproject")
     return out
+
+
+# ---- generic band pipeline (affine / rectify host paths) --------------------------
+class _SourceRows:
+    """Host -> device copies of source rows on demand: only rows not yet
+    resident are copied (in contiguous runs, every dim-0 slice), on `stream`."""
+
+    def __init__(self, src: np.ndarray, dsrc, stream):
+        self.src, self.dsrc, self.stream = src, dsrc, stream
+        self.resident = np.zeros(src.shape[1], bool)
+        self.row_bytes = src.shape[2] * src.itemsize
+
+    def need(self, j0: int, j1: int) -> None:
+        j0, j1 = max(0, int(j0)), min(len(self.resident), int(j1))
+        if j1 <= j0:
+            return
+        missing = np.concatenate([[0], (~self.resident[j0:j1]).astype(np.int8), [0]])
+        edges = np.flatnonzero(np.diff(missing))
+        for a, b in zip(edges[0::2], edges[1::2]):
+            ra, rb = j0 + int(a), j0 + int(b)
+            for s in range(self.src.shape[0]):
+                _copy(self.dsrc[s, ra].data_ptr(), self.src[s, ra:rb].ctypes.data,
+                      (rb - ra) * self.row_bytes, self.stream)
+        self.resident[j0:j1] = True
+
+
+def band_pipeline(src: np.ndarray, dsrc, out: np.ndarray, bands, src_rows, launch,
+                  device, poison: bool = False) -> np.ndarray:
+    """The three-stream pattern of `reproject_host` for any kernel whose target
+    row band [r0, r1) reads only source rows [j0, j1):
+
+        copy-in  : the band's source rows not yet resident -> dsrc
+        kernel   : launch(b, r0, r1, buf, stream) writes the band into buf
+        copy-out : buf -> out[:, r0:r1]
+
+    `src` / `out` are C-contiguous host arrays (n, H, W) / (n, H', W'),
+    page-locked in place for the duration.  ``poison`` (tests): fill the device
+    source with NaN bytes first, so a kernel that read a row outside its band's
+    [j0, j1) would not match the resident result."""
+    t = torch()
+    n, hd, wd = out.shape
+    band_max = max(r1 - r0 for r0, r1 in bands)
+    out_dtype = out.dtype
+    bufs = [empty((n, band_max, wd), out_dtype, device) for _ in range(2)]
+    if poison:
+        dsrc.view(t.uint8).fill_(0xFF)
+    cur = t.cuda.current_stream(device)
+    s_in, s_k, s_out = (t.cuda.Stream(device) for _ in range(3))
+    for s in (s_in, s_k, s_out):
+        s.wait_stream(cur)
+    rows = _SourceRows(src, dsrc, s_in)
+    row_dst = wd * out_dtype.itemsize
+    freed: list = [None, None]
+    with HostPin(src), HostPin(out):
+        try:
+            for b, ((r0, r1), (j0, j1)) in enumerate(zip(bands, src_rows)):
+                rows.need(j0, j1)
+                ev_in = t.cuda.Event()
+                ev_in.record(s_in)
+                s_k.wait_event(ev_in)
+                if freed[b % 2] is not None:   # the copy-out of band b-2 has drained
+                    s_k.wait_event(freed[b % 2])
+                buf = bufs[b % 2][:, :r1 - r0]
+                launch(b, r0, r1, buf, s_k)
+                ev_k = t.cuda.Event()
+                ev_k.record(s_k)
+                s_out.wait_event(ev_k)
+                for s in range(n):
+                    _copy(out[s, r0:r1].ctypes.data, buf[s].data_ptr(), (r1 - r0) * row_dst,
+                          s_out)
+                freed[b % 2] = t.cuda.Event()
+                freed[b % 2].record(s_out)
+        finally:   # never unpin (or free) while a copy may still be in flight
+            s_in.synchronize()
+            s_k.synchronize()
+            s_out.synchronize()
+    return out
+
+
+def _band_rows(height: int, row_bytes: int, unit: int, target_bytes: int = 64 << 20) -> int:
+    """Rows per band: about `target_bytes` of output, a multiple of `unit`."""
+    rows = max(unit, (target_bytes // max(1, row_bytes)) // unit * unit)
+    return min(rows, -(-height // unit) * unit)
+
+
+def rectify_host(src: np.ndarray, ij, interp: str, fill, device=None,
+                 band_rows: int | None = None, out: np.ndarray | None = None,
+                 poison: bool = False) -> np.ndarray:
+    """K6 over a host-resident (n, H, W) variable into a host (n, H', W')
+    result, streamed in target row bands (rectify.py:297-298: numpy in, numpy
+    out).  Each band needs the source rows its positions ij read: K6 reads rows
+    int(j) and int(j) + 1 (rectify.py:663-734), bounded per target row from ij
+    on the device.  Same values as ``kernels.rectify_var`` on a resident copy."""
+    t = torch()
+    device = require_device(device)
+    src = np.ascontiguousarray(src)
+    n, h, w = src.shape
+    _, hd, wd = ij.shape
+    if out is None:
+        out = np.empty((n, hd, wd), src.dtype)
+    jf = ij[1]
+    nan = t.isnan(jf)
+    lo = t.where(nan, t.full_like(jf, np.inf), jf).amin(dim=1)
+    hi = t.where(nan, t.full_like(jf, -np.inf), jf).amax(dim=1)
+    lo, hi = lo.cpu().numpy(), hi.cpu().numpy()
+    rows = int(band_rows or _band_rows(hd, n * wd * src.itemsize, 8))
+    bands = band_ranges(hd, rows)
+    src_rows = []
+    for r0, r1 in bands:
+        blo, bhi = lo[r0:r1].min(), hi[r0:r1].max()
+        if not np.isfinite(blo):   # nothing to sample: fill only
+            src_rows.append((0, 0))
+        else:
+            src_rows.append((int(np.floor(blo)), int(np.floor(bhi)) + 2))
+    dsrc = empty((n, h, w), src.dtype, device)
+
+    def launch(b, r0, r1, buf, stream):
+        kernels.rectify_var(ij, dsrc, interp, fill, stream=stream, rows=(r0, r1), out=buf)
+
+    return band_pipeline(src, dsrc, out, bands, src_rows, launch, device, poison)
+
+
+def affine_host(src: np.ndarray, plan, device=None, band_chunks: int | None = None,
+                out: np.ndarray | None = None, poison: bool = False) -> np.ndarray | None:
+    """K2 / K3 over a host-resident (nt, H, W) array into a host result,
+    streamed in bands of whole output chunk rows (affine.py:227-228: numpy in,
+    numpy out).  A band of y-chunks [k0, k1) reads only the dask-image input
+    slices of those chunks, rows [rel_y[k], rel_y[k] + len_y[k]); its launch is
+    the plan restricted to those chunks (every output pixel depends only on its
+    chunk's tables, so the values equal the whole launch's).  Returns None when
+    the plan cannot be banded (a separate coarsen pass, or chunks that do not
+    hold whole coarsen windows)."""
+    import dataclasses
+
+    if plan.post_agg is not None or plan.chunk_y % plan.div_y != 0:
+        return None
+    device = require_device(device)
+    src = np.ascontiguousarray(src)
+    nt, h, w = src.shape
+    out_dtype = np.dtype(plan.out_dtype)
+    if out_dtype == np.uint64:
+        return None
+    if out is None:
+        out = np.empty((nt, plan.out_h, plan.out_w), out_dtype)
+    nchunks = len(plan.rel_y)
+    rows_per_chunk = plan.chunk_y // plan.div_y        # output rows of a full y-chunk
+    per = int(band_chunks or max(1, _band_rows(plan.out_h, nt * plan.out_w * out_dtype.itemsize,
+                                               rows_per_chunk) // rows_per_chunk))
+    bands, src_rows, plans = [], [], []
+    for k0 in range(0, nchunks, per):
+        k1 = min(nchunks, k0 + per)
+        r0 = k0 * rows_per_chunk
+        r1 = min(plan.out_h, k1 * rows_per_chunk)
+        bands.append((r0, r1))
+        src_rows.append((int(plan.rel_y[k0:k1].min()),
+                         int((plan.rel_y[k0:k1] + plan.len_y[k0:k1]).max())))
+        plans.append(dataclasses.replace(plan, out_h=r1 - r0, rel_y=plan.rel_y[k0:k1],
+                                         len_y=plan.len_y[k0:k1], off_y=plan.off_y[k0:k1],
+                                         _cache={}))
+    for p in plans:   # small tables, uploaded before the streams start
+        p.device_tables(device)
+    kernels.reserve_affine_workspace(device, max(p.out_h for p in plans) * plan.div_y,
+                                     plan.out_w * plan.div_x)
+    dsrc = empty((nt, h, w), src.dtype, device)
+
+    def launch(b, r0, r1, buf, stream):
+        kernels.affine(dsrc, plans[b], out=buf, stream=stream)
+
+    return band_pipeline(src, dsrc, out, bands, src_rows, launch, device, poison)
