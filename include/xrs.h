@@ -300,12 +300,15 @@ int xrs_rectify_var(const double* ij, int64_t ij_sn, int64_t dst_h, int64_t dst_
  *                                         generic K3 instead of K3i
  *   XRS_TESTING_RECTIFY_EXACT             1: K5 decides every triangle test and
  *                                         pixel floor by the exact division
+ *   XRS_TESTING_RECTIFY_MARGIN            k > 1: K5 widens its float32 form margin
+ *                                         k-fold (more pixels take the exact test)
  * Returns the previous value (or XRS_ERR_ARG for an unknown knob).
  * ------------------------------------------------------------------------- */
 #define XRS_TESTING_REPROJECT_BAND 1
 #define XRS_TESTING_REPROJECT_BLOCKS_PER_CU 2
 #define XRS_TESTING_AFFINE_GENERIC 3
 #define XRS_TESTING_RECTIFY_EXACT 4
+#define XRS_TESTING_RECTIFY_MARGIN 5
 #define XRS_TESTING_NUM_KNOBS 8
 int64_t xrs_testing_set(int knob, int64_t value);
 

@@ -389,3 +389,76 @@ def test_nan_cornered_quads_on_untiled_large_target():
     np.testing.assert_array_equal(bb, exp_bb)
     assert_bitwise_equal(ij.cpu().numpy(), exp_ij, "ij")
     assert np.isfinite(exp_ij[0]).sum() > 0.5 * size[0] * size[1]
+
+
+def _device_ij_crs(x, y, size, tile, xy_min, res, j_up, crs, names):
+    import xcube_resampling_amd as xrs
+    from xcube_resampling_amd import rectify as R
+
+    tgm = xrs.GridMapping.regular(size, xy_min, res, crs, tile_size=tile, is_j_axis_up=j_up)
+    sgm = xrs.GridMapping.from_coords(xrs.DataArray(x, ("y", "x"), name=names[0]),
+                                      xrs.DataArray(y, ("y", "x"), name=names[1]), crs)
+    _, _, bb, _ = R.rectify_tiles(sgm, tgm)
+    return R._compute_target_source_ij(sgm, tgm, 1e-3), bb
+
+
+# quads covering ~0.3 to ~4 target pixels per side, rotated and sheared, in
+# degrees near (5, 60) and in UTM metres near (5e5, 6.6e6) with 20-30 m pixels
+FORM_CASES = [
+    # (seed, scale, angle_deg, projected, jitter, j_up)
+    (0, 0.35, 0.0, False, 0.05, False),
+    (1, 0.9, 17.0, False, 0.2, True),
+    (2, 1.6, -33.0, True, 0.05, False),
+    (3, 2.4, 61.0, True, 0.3, False),
+    (4, 3.7, 5.0, False, 0.0, False),
+    (5, 1.0, 0.0, True, 0.0, True),    # lattice: source points on target pixel centres
+]
+
+
+def _form_case_geometry(seed, scale, angle, projected, jitter):
+    rng = np.random.default_rng(100 + seed)
+    h, w = 150, 170
+    res = 25.0 if projected else 0.0025
+    src_res = res * scale
+    jj, ii = np.mgrid[0:h, 0:w].astype(np.float64)
+    c, s = np.cos(np.radians(angle)), np.sin(np.radians(angle))
+    u = (ii + 0.5) * src_res
+    v = (jj + 0.5) * src_res
+    x0, y0 = (500000.0, 6600000.0) if projected else (5.0, 60.0)
+    x = x0 + c * u + s * v + rng.normal(0, jitter * src_res, (h, w))
+    y = y0 - (-s * u + c * v) + rng.normal(0, jitter * src_res, (h, w))
+    gx0 = float(np.floor(np.nanmin(x) / res) * res)
+    gy0 = float(np.floor(np.nanmin(y) / res) * res)
+    if jitter == 0.0 and angle == 0.0 and scale == 1.0:   # lattice: centres coincide
+        x = gx0 + (ii + 0.5) * res
+        y = gy0 + (h - jj - 0.5) * res
+    size = (int(np.ceil((np.nanmax(x) - gx0) / res)) + 1,
+            int(np.ceil((np.nanmax(y) - gy0) / res)) + 1)
+    return x, y, size, (gx0, gy0), res
+
+
+@pytest.mark.parametrize("seed,scale,angle,projected,jitter,j_up", FORM_CASES)
+def test_claim_forms_match_oracle_geometries(seed, scale, angle, projected, jitter, j_up):
+    """K5a decides each (quad, pixel) test from float32 affine forms with a
+    per-quad error bound and the reference's exact float64 test inside the
+    band: over quads from 0.35 to 3.7 target pixels wide, rotated, jittered,
+    in degrees and in UTM metres (large coordinates, small pixels), and a
+    lattice whose source points sit on target pixel centres, ij == the C
+    oracle bit for bit — and again with the band widened 3000-fold (the
+    exact-test path taken by a large share of the tests)."""
+    from oracle import gridmapping_ref as gref
+    from xcube_resampling_amd._native import testing_knob
+
+    x, y, size, xy_min, res = _form_case_geometry(seed, scale, angle, projected, jitter)
+    tile = (64, 48)
+    crs, names = ("EPSG:32632", ("x", "y")) if projected else ("EPSG:4326", ("lon", "lat"))
+    geo = gref.regular_geometry(size, xy_min, res, tile_size=tile, is_j_axis_up=j_up)
+    exp_ij, exp_bb = rectify_ref.compute_target_source_ij(x, y, size, tile, geo["xy_bbox"],
+                                                          geo["xy_res"], j_up, threads=8)
+    assert np.isfinite(exp_ij[0]).sum() > 0.3 * size[0] * size[1]
+    ij, bb = _device_ij_crs(x, y, size, tile, xy_min, res, j_up, crs, names)
+    np.testing.assert_array_equal(bb, exp_bb)
+    assert_bitwise_equal(ij.cpu().numpy(), exp_ij, "ij")
+    with testing_knob("rectify_margin", 3000):
+        ij_w, _ = _device_ij_crs(x, y, size, tile, xy_min, res, j_up, crs, names)
+    assert_bitwise_equal(ij_w.cpu().numpy(), exp_ij, "ij (widened band)")

@@ -192,6 +192,19 @@ inline int grid_blocks(int64_t nwork, int per_block, int cap) {
   return (int)nb;
 }
 
+// Blocks of `kernel` resident on the whole device at once (occupancy per CU x
+// CU count), for grids that deal work round-robin and must not leave a tail
+// of blocks that start only when others end.
+inline int resident_blocks(const void* kernel, int threads, size_t dyn_lds = 0) {
+  int dev = 0, cus = 0, per_cu = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, dyn_lds) !=
+          hipSuccess)
+    return 256 * 4;
+  return (per_cu > 0 ? per_cu : 1) * (cus > 0 ? cus : 1);
+}
+
 }  // namespace xrs
 
 // Thread-local error message reported through xrs_last_error().

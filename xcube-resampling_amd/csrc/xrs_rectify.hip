@@ -255,7 +255,8 @@ struct RectArgs {
   double uv_delta;
   double inv_x, inv_y;         // 1 / x_scale, 1 / y_scale (claim fast paths)
   double margin;               // window floors: relative margin (inf: always exact)
-  double uv_margin;            // triangle tests: margin in u units (inf: always exact)
+  int exact;                   // 1: the reference's exact test at every pixel (tests)
+  float margin_scale;          // form margin factor (tests: >1 widens the exact-test band)
   uint32_t* keys;              // (dst_h, dst_w) claim keys, 0xFFFFFFFF = free
   double* ij;                  // (2, dst_h, dst_w) output
 };
@@ -318,10 +319,17 @@ constexpr double kMargin = 1e-9;
 // ---- K5a: claim target pixels with the raster-order key of hitting quads -------
 // Work item ("strip") = kStripH quad rows x kStripW quads of one tile's source
 // window, walked by ONE wave: lane l owns point column l of the strip (64
-// points = 63 quads), so each source point is loaded and scaled to target
-// pixel units once per strip row; the quad to its right takes the right-hand
-// corners from the next lane (DPP wave shift) and, walking down, a row's
-// bottom corners become the next row's top corners in registers.
+// points = 63 quads), so each source point is loaded once per strip row (the
+// next row's points are requested before this row's tests); the quad to its
+// right takes the right-hand corners from the next lane (DPP wave shift) and,
+// walking down, a row's bottom corners become the next row's top corners in
+// registers.  Strips are dealt round-robin to the waves of a grid sized to be
+// resident at once (no tail of late blocks).  A dynamic work counter costs
+// more than it balances: one global atomic per strip on one address
+// serialises at its L2 channel (measured 0.45 vs 0.12 ms for the bare strip
+// loop at config 4); staging a strip's points in LDS (rows then never wait on
+// the claim atomics in flight) limits the grid to 2 waves per SIMD and was
+// slower.
 //
 // Window.  The reference tests every pixel of the window spanned by the
 // floors of the four corners' pixel coordinates (rectify.py:500-526); floor is
@@ -331,13 +339,19 @@ constexpr double kMargin = 1e-9;
 //
 // Tests.  Per triangle (A = p0 p1 p2, B = p3 p2 p1) the reference computes
 // nu = _fu(...), nv = _fv(...) (rectify.py:737-768), u = nu / det, v = nv /
-// det and hits when u >= umin, v >= umin, u + v <= uvmax.  The quad hoists
-// the corner differences inside _fdet / _fu / _fv (the same float64
-// operations, so det and every numerator are bit-identical to the
-// reference's) and walks its clipped window in its own lane; u and v come
-// from the reciprocal of det when clearly (kUvMargin) away from every limit,
-// else from the reference's divisions, so every hit / miss equals the
-// reference's.  Hits are claimed with a global atomicMin of the quad's key.
+// det at every pixel centre of the window and hits when u >= umin, v >= umin,
+// u + v <= uvmax.  In exact arithmetic u, v and u + v are affine in the
+// window position (a, b): u = U0 + a Ui + b Uj.  The quad evaluates the three
+// forms of both triangles in float32 (two FMAs each), shifted so that a hit is
+// min3(u', v', s') >= 0, with a per-quad bound M on |form - the reference's
+// float64 value| (float32 evaluation + conversion of the coefficients, plus
+// the reference's own rounding of dx, ex, nu, u: LinQuad::setup).  A pixel is
+// decided by the forms when max over the triangles of min3 is >= 0 (some
+// triangle surely hits) or < -2M (every triangle surely misses), else — a
+// pixel centre within M of a triangle edge, rare — by the reference's exact
+// float64 test (tri_exact), so every hit / miss equals the reference's.  A
+// quad with a non-finite corner or a large M takes the exact test at every
+// pixel.  Hits are claimed with a global atomicMin of the quad's key.
 //
 // Windows larger than kLaneWindow (a quad with a NaN corner spans its whole
 // tile, rectify.py:500-526) are walked by the whole wave, 64 pixels per step,
@@ -345,42 +359,61 @@ constexpr double kMargin = 1e-9;
 // synchronisation after the offsets are staged).
 // Work list: chunk c belongs to the tile t with offs[t] <= c < offs[t+1] (the
 // offsets come from xrs_rectify_tiles on the device, or from the host).
-constexpr int kOffsLds = 2047;   // tiles whose offsets are copied to LDS (16 KB)
+constexpr int kClaimThreads = 256;   // K5a block: 4 waves
+constexpr int kClaimOffsLds = 1023;  // tiles whose offsets are copied to LDS (8 KB)
 constexpr int kLaneWindow = 16;  // windows up to this many pixels: walked per lane
-constexpr double kUvMargin = 1e-9;
+constexpr double kEps64 = 0x1p-52;
+constexpr double kEps32 = 0x1p-23;
+constexpr double kMaxFormMargin = 1e-3;   // larger bound: exact test at every pixel
 
-struct QuadEdges {     // both triangles of a quad, hoisted for the pixel tests
-  double x0, y0, au1, au2, av1, av2, det_a, r_a;   // A = (p0, p1, p2)
-  double x3, y3, bu1, bu2, bv1, bv2, det_b, r_b;   // B = (p3, p2, p1)
+// One triangle's three affine forms over the quad's pixel window (float32)
+// and the decision threshold thr = -2M.  form(a, b) = c0 + a ci + b cj.
+struct TriForms {
+  float c[9];   // (c0, ci, cj) of u - umin - M, v - umin - M, uvmax - M - (u + v)
+  float thr;
 };
 
-// hit / no hit of one triangle from its numerators nu = _fu(...), nv =
-// _fv(...) (bit-identical to the reference's: the same float64 operations on
-// the same hoisted differences): decided by the reciprocal when every value
-// is clearly away from its limit, by the reference's divisions otherwise
-// (|u - nu/det| <= ~3 ulp(u): below the margin for |u| < 1e5, and beyond that
-// u is farther than its error from every limit — an absolute margin suffices)
-__device__ inline bool tri_decide(double nu, double nv, double det, double r, double umin,
-                                  double uvmax, double margin) {
-  if (det == 0.0) return false;
-  const double u = nu * r, v = nv * r, s = u + v;
-  if (fabs(u - umin) > margin && fabs(v - umin) > margin && fabs(s - uvmax) > margin)
-    return u >= umin && v >= umin && s <= uvmax;
-  const double ue = nu / det, ve = nv / det;
-  return ue >= umin && ve >= umin && ue + ve <= uvmax;
-}
-
-// rectify.py:556-573 for the target pixel centre (dx, dy): triangle A, then B
-__device__ inline bool quad_covers(const QuadEdges& e, double dx, double dy, double umin,
-                                   double uvmax, double margin) {
-  double ex = e.x0 - dx, ey = e.y0 - dy;
-  if (tri_decide(ex * e.au1 - ey * e.au2, ey * e.av1 - ex * e.av2, e.det_a, e.r_a, umin, uvmax,
-                 margin))
-    return true;
-  ex = e.x3 - dx;
-  ey = e.y3 - dy;
-  return tri_decide(ex * e.bu1 - ey * e.bu2, ey * e.bv1 - ex * e.bv2, e.det_b, e.r_b, umin,
-                    uvmax, margin);
+// One triangle's forms over the window, evaluated in float32 (window position
+// (0, 0) = the pixel centre at which the corner differences (ex, ey) are
+// taken, in float64 exactly as the reference takes them).  e1..e4: the edge
+// factors of _fu(p, c, q) = ex e1 - ey e2 and _fv(p, c, r) = ey e3 - ex e4
+// (rectify.py:745-768); det = _fdet(...) != 0; the pixel centre moves by
+// (sx, sy) per column / row (ex -= sx, ey -= sy).  M bounds |form - the
+// reference's float64 value| over the window:
+//   float32: the inputs rounded to float (ex, ey, e, det), the reciprocal
+//     (1 ulp), the products and sums of u0, v0 (terms pu, pv), of the steps,
+//     and the two FMAs over the window (T, g): <= E eps32, with a factor >= 2
+//     to spare in every term
+//   reference: dx = x_off + (i + 0.5) sx and ex = x0 - dx round by
+//     <= eps64 (3 X + |x0|), X = |x_off| + (tw + 1) |sx|; the products of nu
+//     by eps64 |ex e|; u = nu / det by eps64 |u|: <= 5 eps64 R + eps64 T
+// M = 2 (E eps32 + 10 eps64 R + 8 eps64 T), evaluated in float32 and scaled
+// up by 1.01 for its own rounding.  Returns false (every pixel of the window
+// to the exact test) when M is NaN / inf or above kMaxFormMargin (degenerate
+// triangles).
+__device__ inline bool tri_setup(double ex64, double ey64, double e1_64, double e2_64,
+                                 double e3_64, double e4_64, double det, float sx, float sy,
+                                 float X, float Y, float ax, float ay, float wn, float hn,
+                                 float umin, float uvmax, float margin_scale, TriForms& F) {
+  const float ex = (float)ex64, ey = (float)ey64;
+  const float e1 = (float)e1_64, e2 = (float)e2_64, e3 = (float)e3_64, e4 = (float)e4_64;
+  const float r = __builtin_amdgcn_rcpf((float)det), ar = fabsf(r);
+  const float pu = (fabsf(ex * e1) + fabsf(ey * e2)) * ar;   // |terms| of u0
+  const float pv = (fabsf(ey * e3) + fabsf(ex * e4)) * ar;
+  const float u0 = (ex * e1 - ey * e2) * r, v0 = (ey * e3 - ex * e4) * r;
+  const float ui = -sx * e1 * r, uj = sy * e2 * r, vi = sx * e4 * r, vj = -sy * e3 * r;
+  const float g = wn * (fabsf(ui) + fabsf(vi)) + hn * (fabsf(uj) + fabsf(vj));
+  const float T = fabsf(u0) + fabsf(v0) + g;
+  const float E = 10.0f * (pu + pv) + 8.0f * g + 6.0f * (T + 4.0f);
+  const float R = ((X + ax) * (fabsf(e1) + fabsf(e4)) + (Y + ay) * (fabsf(e2) + fabsf(e3))) * ar;
+  const float M = 2.02f * ((float)kEps32 * E + 10.0f * (float)kEps64 * R +
+                           8.0f * (float)kEps64 * T) * margin_scale;
+  if (!(M <= (float)kMaxFormMargin * margin_scale)) return false;
+  F.c[0] = (u0 - umin) - M; F.c[1] = ui; F.c[2] = uj;
+  F.c[3] = (v0 - umin) - M; F.c[4] = vi; F.c[5] = vj;
+  F.c[6] = (uvmax - (u0 + v0)) - M; F.c[7] = -(ui + vi); F.c[8] = -(uj + vj);
+  F.thr = -2.0f * M;
+  return true;
 }
 
 // the reference's test of one triangle at pixel centre (dx, dy)
@@ -444,19 +477,56 @@ __device__ inline Quad load_quad32(const RectArgs& a, int32_t qj, int32_t qi) {
   return load_quad(a, qj, qi);
 }
 
-__global__ void __launch_bounds__(kThreads)
+__device__ inline float min3f(float x, float y, float z) { return fminf(x, fminf(y, z)); }
+
+// A quad the fast path cannot take (a non-finite corner, a pixel-unit extreme
+// close to an integer, a degenerate quad, the test knob): the reference's
+// window (rectify.py:500-526, exact divisions) and, for windows up to
+// kLaneWindow, its exact test at every pixel; larger windows are handed back
+// (imin, jmin, nw, big_cnt) for the wave-wide walk.
+__device__ inline void claim_exact_lane(const RectArgs& a, const TileInfo& ti, int32_t qj,
+                                              int32_t qi, uint32_t key, double umin,
+                                              double uvmax, int32_t& imin, int32_t& jmin,
+                                              int32_t& nw, int64_t& big_cnt) {
+  const Quad Q = load_quad(a, qj, qi);
+  int64_t i0, i1, j0, j1;
+  pix_range_exact(Q.x0, Q.x1, Q.x2, Q.x3, ti.x_off, a.x_scale, i0, i1);
+  pix_range_exact(Q.y0, Q.y1, Q.y2, Q.y3, ti.y_off, a.y_scale, j0, j1);
+  if (i1 < 0 || j1 < 0 || i0 >= ti.tw || j0 >= ti.th) return;
+  i0 = max(i0, (int64_t)0); j0 = max(j0, (int64_t)0);
+  i1 = min(i1, (int64_t)ti.tw - 1); j1 = min(j1, (int64_t)ti.th - 1);
+  double det_a, det_b;
+  quad_dets(Q, det_a, det_b);
+  if (det_a == 0.0 && det_b == 0.0) return;
+  const int32_t w = (int32_t)(i1 - i0 + 1), h = (int32_t)(j1 - j0 + 1);
+  const int64_t cnt = (int64_t)w * h;
+  if (cnt > kLaneWindow) {
+    imin = (int32_t)i0; jmin = (int32_t)j0; nw = w; big_cnt = cnt;
+    return;
+  }
+  for (int32_t dj = (int32_t)j0; dj <= (int32_t)j1; ++dj) {
+    const double dy = ti.y_off + ((double)dj + 0.5) * a.y_scale;
+    for (int32_t di = (int32_t)i0; di <= (int32_t)i1; ++di) {
+      const double dx = ti.x_off + ((double)di + 0.5) * a.x_scale;
+      if (tri_exact(Q, false, dx, dy, umin, uvmax) || tri_exact(Q, true, dx, dy, umin, uvmax))
+        atomicMin(a.keys + (int64_t)(ti.r0 + dj) * a.dst_w + ti.c0 + di, key);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(kClaimThreads)
 rectify_claim_kernel(RectArgs a) {
-  __shared__ int64_t offs_s[kOffsLds + 1];
+  __shared__ int64_t offs_s[kClaimOffsLds + 1];
   const int lane = threadIdx.x & 63;
-  const bool lds_offs = a.ntiles <= kOffsLds;
+  const bool lds_offs = a.ntiles <= kClaimOffsLds;
   if (lds_offs)
-    for (int64_t t = threadIdx.x; t <= a.ntiles; t += kThreads) offs_s[t] = a.chunk_offs[t];
+    for (int64_t t = threadIdx.x; t <= a.ntiles; t += kClaimThreads) offs_s[t] = a.chunk_offs[t];
   __syncthreads();
   const int64_t* offs = lds_offs ? offs_s : a.chunk_offs;
   const int64_t nchunks = offs[a.ntiles];
   const double umin = -a.uv_delta, uvmax = 1.0 + 2 * a.uv_delta;
-  const int64_t nwaves = (int64_t)gridDim.x * (kThreads / 64);
-  for (int64_t c = (int64_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6); c < nchunks;
+  const int64_t nwaves = (int64_t)gridDim.x * (kClaimThreads / 64);
+  for (int64_t c = (int64_t)blockIdx.x * (kClaimThreads / 64) + (threadIdx.x >> 6); c < nchunks;
        c += nwaves) {
     int64_t lo = 0, hi = a.ntiles;   // last t with offs[t] <= c
     while (hi - lo > 1) {
@@ -473,7 +543,8 @@ rectify_claim_kernel(RectArgs a) {
     const bool has_pt = pcol <= nq_i;
     const bool has_q = lane < kStripW && pcol < nq_i;  // quad (row, pcol) exists
     const int32_t qi = ti.si0 + pcol;
-    const int32_t r_end = min(cy * kStripH + kStripH, nq_j);
+    const int32_t r0 = cy * kStripH;
+    const int32_t r_end = min(r0 + kStripH, nq_j);
     auto load_pt = [&](int32_t qj) {
       StripPoint p{NAN, NAN};
       if (has_pt) {
@@ -486,16 +557,20 @@ rectify_claim_kernel(RectArgs a) {
     // target pixel units by the reciprocal (window floors)
     auto qx = [&](double x) { return (x - ti.x_off) * a.inv_x; };
     auto qy = [&](double y) { return (y - ti.y_off) * a.inv_y; };
-    StripPoint t0 = load_pt(ti.sj0 + cy * kStripH);
+    StripPoint t0 = load_pt(ti.sj0 + r0);
     StripPoint t1 = strip_next(t0);
-    for (int32_t r = cy * kStripH; r < r_end; ++r) {
+    StripPoint nxt = load_pt(ti.sj0 + r0 + 1);
+    for (int32_t r = r0; r < r_end; ++r) {
       const int32_t qj = ti.sj0 + r;                    // global quad row (corner p0)
-      const StripPoint b0 = load_pt(qj + 1);
+      const StripPoint b0 = nxt;
+      // the next row's bottom points are requested before this row's tests
+      if (r + 1 < r_end) nxt = load_pt(qj + 2);
       const StripPoint b1 = strip_next(b0);
       // corners p0 = t0, p1 = t1, p2 = b0, p3 = b1
-      int64_t cnt = 0;
-      int32_t imin = 0, jmin = 0, nw = 0, nh = 0;
-      QuadEdges e{};
+      int32_t imin = 0, jmin = 0, nw = 0;
+      int64_t big_cnt = 0;   // > 0: window above kLaneWindow, walked by the wave below
+      bool slow = false;     // window not decided fast: claim_exact_lane
+      uint32_t hit = 0, unsure = 0;   // bit k: window pixel k (row-major) hit / undecided
       if (has_q) {
         double fx0, fx1, fy0, fy1;
         // floor is monotone and the reciprocal's error tiny: the extremes of the
@@ -507,59 +582,99 @@ rectify_claim_kernel(RectArgs a) {
         const double qy1 = qy(a.y_scale > 0 ? fmax(fmax(t0.y, t1.y), fmax(b0.y, b1.y))
                                             : fmin(fmin(t0.y, t1.y), fmin(b0.y, b1.y)));
         const double fin = t0.x + t1.x + b0.x + b1.x + t0.y + t1.y + b0.y + b1.y;
-        int64_t i0, i1, j0, j1;
         if (fin - fin == 0.0 && fmax(fabs(qx0), fabs(qx1)) < 0x1p40 &&
             fmax(fabs(qy0), fabs(qy1)) < 0x1p40 && floor_clear(qx0, a.margin, fx0) &&
             floor_clear(qx1, a.margin, fx1) && floor_clear(qy0, a.margin, fy0) &&
             floor_clear(qy1, a.margin, fy1)) {
-          i0 = (int64_t)fx0; i1 = (int64_t)fx1; j0 = (int64_t)fy0; j1 = (int64_t)fy1;
-        } else {
-          pix_range_exact(t0.x, t1.x, b0.x, b1.x, ti.x_off, a.x_scale, i0, i1);
-          pix_range_exact(t0.y, t1.y, b0.y, b1.y, ti.y_off, a.y_scale, j0, j1);
-        }
-        if (!(i1 < 0 || j1 < 0 || i0 >= ti.tw || j0 >= ti.th)) {
-          i0 = max(i0, (int64_t)0); j0 = max(j0, (int64_t)0);
-          i1 = min(i1, (int64_t)ti.tw - 1); j1 = min(j1, (int64_t)ti.th - 1);
-          // edge factors = the differences inside the reference's _fdet / _fu / _fv
-          const double au1 = t0.y - b0.y, au2 = t0.x - b0.x;   // _fu(p, p0, p2)
-          const double av1 = t0.x - t1.x, av2 = t0.y - t1.y;   // _fv(p, p0, p1)
-          const double bu1 = b1.y - t1.y, bu2 = b1.x - t1.x;   // _fu(p, p3, p1)
-          const double bv1 = b1.x - b0.x, bv2 = b1.y - b0.y;   // _fv(p, p3, p2)
-          double det_a = av1 * au1 - au2 * av2;   // _fdet(p0, p1, p2)
-          double det_b = bv1 * bu1 - bu2 * bv2;   // _fdet(p3, p2, p1)
-          if (det_a != det_a) det_a = 0.0;
-          if (det_b != det_b) det_b = 0.0;
-          if (!(det_a == 0.0 && det_b == 0.0)) {
-            imin = (int32_t)i0; jmin = (int32_t)j0;
-            nw = (int32_t)(i1 - i0 + 1);
-            nh = (int32_t)(j1 - j0 + 1);
-            cnt = (int64_t)nw * nh;
-            e.x0 = t0.x; e.y0 = t0.y; e.au1 = au1; e.au2 = au2; e.av1 = av1; e.av2 = av2;
-            e.det_a = det_a; e.r_a = det_a != 0.0 ? 1.0 / det_a : 0.0;
-            e.x3 = b1.x; e.y3 = b1.y; e.bu1 = bu1; e.bu2 = bu2; e.bv1 = bv1; e.bv2 = bv2;
-            e.det_b = det_b; e.r_b = det_b != 0.0 ? 1.0 / det_b : 0.0;
+          int32_t i0 = (int32_t)fx0, i1 = (int32_t)fx1, j0 = (int32_t)fy0, j1 = (int32_t)fy1;
+          if (!(i1 < 0 || j1 < 0 || i0 >= ti.tw || j0 >= ti.th)) {
+            i0 = max(i0, 0); j0 = max(j0, 0);
+            i1 = min(i1, ti.tw - 1); j1 = min(j1, ti.th - 1);
+            imin = i0; jmin = j0;
+            nw = i1 - i0 + 1;
+            const int32_t nh = j1 - j0 + 1;
+            const int64_t cnt = (int64_t)nw * nh;
+            if (cnt > kLaneWindow) {
+              big_cnt = cnt;   // (a quad without a triangle is dropped there)
+            } else {
+              const int32_t n = (int32_t)cnt;
+              const uint32_t all = (1u << n) - 1;
+              const double dx0 = ti.x_off + ((double)i0 + 0.5) * a.x_scale;   // pixel (i0, j0)
+              const double dy0 = ti.y_off + ((double)j0 + 0.5) * a.y_scale;
+              const float X = fabsf((float)ti.x_off) + (float)(ti.tw + 1) * fabsf((float)a.x_scale);
+              const float Y = fabsf((float)ti.y_off) + (float)(ti.th + 1) * fabsf((float)a.y_scale);
+              const float wn = (float)(nw - 1), hn = (float)(nh - 1);
+              // one triangle at a time (its forms only are live during its walk)
+              auto walk = [&](double ex, double ey, double e1, double e2, double e3, double e4,
+                              double cx, double cy) -> uint2 {   // (hit, undecided) masks
+                // _fdet of the triangle from its edge factors (NaN -> 0: never hit)
+                const double det = e3 * e1 - e2 * e4;
+                if (det != det || det == 0.0) return uint2{0u, 0u};
+                TriForms F;
+                if (a.exact || !tri_setup(ex, ey, e1, e2, e3, e4, det, (float)a.x_scale,
+                                          (float)a.y_scale, X, Y, fabsf((float)cx),
+                                          fabsf((float)cy), wn, hn, (float)umin, (float)uvmax,
+                                          a.margin_scale, F))
+                  return uint2{0u, all};
+                uint32_t h_hit = 0, h_uns = 0;
+                float af = 0.0f, bf = 0.0f;
+                int32_t col = 0;
+                for (int32_t k = 0; k < n; ++k) {
+                  const float h = min3f(fmaf(bf, F.c[2], fmaf(af, F.c[1], F.c[0])),
+                                        fmaf(bf, F.c[5], fmaf(af, F.c[4], F.c[3])),
+                                        fmaf(bf, F.c[8], fmaf(af, F.c[7], F.c[6])));
+                  const uint32_t bit = 1u << k;
+                  h_hit |= h >= 0.0f ? bit : 0u;
+                  h_uns |= h < 0.0f && h >= F.thr ? bit : 0u;
+                  af += 1.0f;
+                  if (++col == nw) { col = 0; af = 0.0f; bf += 1.0f; }
+                }
+                return uint2{h_hit, h_uns};
+              };
+              // A = (p0, p1, p2): _fu(p, p0, p2), _fv(p, p0, p1), _fdet(p0, p1, p2)
+              const uint2 ma = walk(t0.x - dx0, t0.y - dy0, t0.y - b0.y, t0.x - b0.x,
+                                    t0.x - t1.x, t0.y - t1.y, t0.x, t0.y);
+              // B = (p3, p2, p1): _fu(p, p3, p1), _fv(p, p3, p2), _fdet(p3, p2, p1)
+              const uint2 mb = walk(b1.x - dx0, b1.y - dy0, b1.y - t1.y, b1.x - t1.x,
+                                    b1.x - b0.x, b1.y - b0.y, b1.x, b1.y);
+              hit = ma.x | mb.x;
+              unsure = ma.y | mb.y;
+              unsure &= ~hit;
+            }
           }
+        } else {
+          slow = true;
         }
       }
       const uint32_t key = (uint32_t)qj * (uint32_t)a.w + (uint32_t)qi;
-      // small windows: every lane walks its own
-      {
-        const int32_t n = cnt <= kLaneWindow ? (int32_t)cnt : 0;
-        int32_t di = imin, dj = jmin;
-        uint32_t* row = a.keys + (int64_t)(ti.r0 + dj) * a.dst_w + ti.c0;
-        for (int32_t k = 0; k < n; ++k) {
-          const double dy = ti.y_off + ((double)dj + 0.5) * a.y_scale;
-          const double dx = ti.x_off + ((double)di + 0.5) * a.x_scale;
-          if (quad_covers(e, dx, dy, umin, uvmax, a.uv_margin)) atomicMin(row + di, key);
-          if (++di == imin + nw) {
-            di = imin;
-            ++dj;
-            row += a.dst_w;
-          }
+      // claims: the window pixels hit (row k / nw, column k % nw: exact in float
+      // for k < 16, the quotient is >= 1/32 from an integer)
+      if (hit | unsure) {
+        const float rnw = 1.0f / (float)nw;
+        uint32_t* tile_keys = a.keys + (int64_t)ti.r0 * a.dst_w + ti.c0;
+        while (hit) {
+          const int k = __builtin_ctz(hit);
+          hit &= hit - 1;
+          const int32_t dj = (int32_t)(((float)k + 0.5f) * rnw);
+          atomicMin(tile_keys + (int64_t)(jmin + dj) * a.dst_w + imin + k - dj * nw, key);
+        }
+        if (unsure) {   // a pixel centre within the margin of an edge: the reference's test
+          const Quad Q = load_quad(a, qj, qi);
+          do {
+            const int k = __builtin_ctz(unsure);
+            unsure &= unsure - 1;
+            const int32_t dj = (int32_t)(((float)k + 0.5f) * rnw);
+            const int32_t di = imin + k - dj * nw;
+            const double dy = ti.y_off + ((double)(jmin + dj) + 0.5) * a.y_scale;
+            const double dx = ti.x_off + ((double)di + 0.5) * a.x_scale;
+            if (tri_exact(Q, false, dx, dy, umin, uvmax) || tri_exact(Q, true, dx, dy, umin, uvmax))
+              atomicMin(tile_keys + (int64_t)(jmin + dj) * a.dst_w + di, key);
+          } while (unsure);
         }
       }
+      if (slow) claim_exact_lane(a, ti, qj, qi, key, umin, uvmax, imin, jmin, nw, big_cnt);
       // large windows: one quad at a time, walked by the whole wave (exact test)
-      uint64_t big = __ballot(cnt > kLaneWindow);
+      uint64_t big = __ballot(big_cnt > 0);
       while (big) {
         const int o = __builtin_ctzll(big);
         big &= big - 1;
@@ -570,8 +685,8 @@ rectify_claim_kernel(RectArgs a) {
         const int32_t wnw = __builtin_amdgcn_readlane(nw, o);
         const uint32_t wkey = __builtin_amdgcn_readlane(key, o);
         const int64_t wcnt =
-            ((int64_t)__builtin_amdgcn_readlane((uint32_t)(cnt >> 32), o) << 32) |
-            __builtin_amdgcn_readlane((uint32_t)cnt, o);
+            ((int64_t)__builtin_amdgcn_readlane((uint32_t)(big_cnt >> 32), o) << 32) |
+            __builtin_amdgcn_readlane((uint32_t)big_cnt, o);
         // test k = lane + 64 s sits at (row k / wnw, column k % wnw), stepped exactly
         const int32_t step_r = 64 / wnw, step_c = 64 % wnw;
         int64_t dj = lane / wnw;
@@ -854,14 +969,22 @@ extern "C" int xrs_rectify_ij(const double* x, const double* y, int64_t h, int64
   // divisions for every decision
   const bool exact = xrs_testing_value(XRS_TESTING_RECTIFY_EXACT) != 0;
   a.margin = exact ? INFINITY : kMargin;
-  a.uv_margin = exact ? INFINITY : kUvMargin;
+  a.exact = exact ? 1 : 0;
+  // tests: xrs_testing_set(XRS_TESTING_RECTIFY_MARGIN, k) widens the form
+  // margin k-fold (more pixels take the exact test; same decisions)
+  const int64_t widen = xrs_testing_value(XRS_TESTING_RECTIFY_MARGIN);
+  a.margin_scale = widen > 1 ? (float)widen : 1.0f;
   hipStream_t st = static_cast<hipStream_t>(stream);
   XRS_HIP_CHECK(hipMemsetAsync(keys, 0xFF, (size_t)(dst_h * dst_w) * sizeof(uint32_t), st));
   {
-    // one strip per wave when the caller knows the strip count, else 8 blocks per CU
-    const int nb = max_chunks > 0 ? grid_blocks(max_chunks, kThreads / 64, 1 << 24)
-                                  : grid_blocks(256 * 8, 1, 1 << 24);
-    hipLaunchKernelGGL(rectify_claim_kernel, dim3(nb), dim3(kThreads), 0, st, a);
+    // as many blocks as are resident at once (fewer when the caller knows a
+    // smaller strip count)
+    constexpr int wpb = kClaimThreads / 64;
+    static const int resident =   // one device model per process
+        resident_blocks(reinterpret_cast<const void*>(rectify_claim_kernel), kClaimThreads);
+    const int64_t want = max_chunks > 0 ? (max_chunks + wpb - 1) / wpb : resident;
+    const int nb = (int)min(want, (int64_t)resident);
+    hipLaunchKernelGGL(rectify_claim_kernel, dim3(nb), dim3(kClaimThreads), 0, st, a);
     XRS_HIP_CHECK(hipGetLastError());
   }
   const int nb2 = grid_blocks(256 * 32, 1, 1 << 24);
