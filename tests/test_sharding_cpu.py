@@ -188,7 +188,7 @@ def _rank_main(rank, world, port, result_dir, balance="rows"):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("balance", ["rows", "bytes"])
+@pytest.mark.parametrize("balance", ["rows", "bytes", "cost"])
 def test_gloo_band_sharded_reprojection_matches_reference(tmp_path, balance):
     """world_size 2 over gloo: each rank holds only the source rows of its
     row band (everything else poisoned), bands split mid-tile, and the

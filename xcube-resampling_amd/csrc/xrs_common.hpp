@@ -94,6 +94,24 @@ __device__ inline XcdSlice xcd_slice(int64_t nwork) {
   return s;
 }
 
+// Group-interleaved variant: the work list is cut into groups of `group`
+// consecutive items and XCD x takes groups x, x + 8, x + 16, ...  For K1 a
+// group is one band of target rows across the raster, so every XCD gets the
+// same mix of cheap and expensive rows (a contiguous slice per XCD left the
+// XCD holding the rows that read the most source rows 6 % behind the others);
+// source-row reuse lives inside a work item, not across bands.
+struct XcdGroups {
+  int64_t xcd, group, nwork, i, step;
+  __device__ inline int64_t item() const {
+    const int64_t m = i / group;
+    return (m * 8 + xcd) * group + (i - m * group);
+  }
+};
+__device__ inline XcdGroups xcd_groups(int64_t nwork, int64_t group) {
+  const int64_t b = blockIdx.x, nb = gridDim.x;  // launcher: nb % 8 == 0
+  return XcdGroups{b % 8, group, nwork, b / 8, nb / 8};
+}
+
 // ---- numpy reduction helpers (K3 / coarsen) --------------------------------
 template <typename T> __device__ inline bool is_nan(T v) { return false; }
 template <> __device__ inline bool is_nan<float>(float v) { return v != v; }

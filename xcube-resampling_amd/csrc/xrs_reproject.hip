@@ -72,6 +72,7 @@ struct Geometry {
   int32_t* err_flags;
   int64_t band;   // target rows per work item of the gathers
   int64_t segw;   // target columns per work item (kThreads x columns per thread)
+  int64_t band_first;   // bands of tile row ty0 above row_begin (not in the work list)
 };
 
 // numpy fancy index on a window axis of length `win` with an int16 index:
@@ -190,14 +191,19 @@ struct GatherArgs {
 };
 
 // Work decomposition shared by K1b/K1c: bands of kBand rows inside one tile row
-// x segments of kSegW columns inside one tile column.  Returns false for empty
-// items (partial edge tiles, rows outside [row_begin, row_end)).
+// x segments of kSegW columns inside one tile column, band-major; the XCDs
+// take whole bands in turn (xcd_groups, group = nsegs).  The list starts at
+// the band holding row_begin and ends at the band holding row_end - 1, so a
+// row band of the raster (a rank's share) has no empty items (blocks are dealt
+// to XCDs round-robin whatever their cost: empty items would idle an XCD).
+// Returns false for empty items (partial edge tiles).
 struct WorkItem {
   int64_t t, ty, tx, r0, r1, c0, c1;
 };
 __device__ inline bool work_item(const Geometry& g, int64_t w, int64_t ty0, int64_t nsegs,
                                  int64_t bands_per_tile, int64_t segs_per_tile, WorkItem& it) {
-  const int64_t b = w / nsegs, s = w - b * nsegs;
+  const int64_t bw = w / nsegs, s = w - bw * nsegs;
+  const int64_t b = bw + g.band_first;
   const int64_t tyi = b / bands_per_tile;
   it.ty = ty0 + tyi;
   const int64_t bi = b - tyi * bands_per_tile;
@@ -222,8 +228,9 @@ gather_separable_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t bands_
                         int64_t segs_per_tile, int64_t nwork) {
   const Geometry& g = a.g;
   const T fill = Conv<T>::from_f64(a.fill);
-  const XcdSlice sl = xcd_slice(nwork);
-  for (int64_t w = sl.first; w < sl.end; w += sl.step) {
+  for (XcdGroups sl = xcd_groups(nwork, nsegs);; sl.i += sl.step) {
+    const int64_t w = sl.item();
+    if (w >= nwork) break;
     WorkItem it;
     if (!work_item(g, w, ty0, nsegs, bands_per_tile, segs_per_tile, it)) continue;
     const AxisEntry* xt = a.xtab + it.t * g.tile_w + (it.c0 - it.tx * g.tile_w);
@@ -298,9 +305,10 @@ gather_2d_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t bands_per_til
                  int64_t segs_per_tile, int64_t nwork) {
   const Geometry& g = a.g;
   const T fill = Conv<T>::from_f64(a.fill);
-  const XcdSlice sl = xcd_slice(nwork);
   int32_t eflags = 0;
-  for (int64_t w = sl.first; w < sl.end; w += sl.step) {
+  for (XcdGroups sl = xcd_groups(nwork, nsegs);; sl.i += sl.step) {
+    const int64_t w = sl.item();
+    if (w >= nwork) break;
     WorkItem it;
     if (!work_item(g, w, ty0, nsegs, bands_per_tile, segs_per_tile, it)) continue;
     const int ncols = (int)(it.c1 - it.c0);
@@ -350,7 +358,11 @@ int launch(const GatherArgs& a, int coord_mode, AxisEntry* xtab, AxisEntry* ytab
   const int64_t bands_per_tile = (g.tile_h + args.g.band - 1) / args.g.band;
   const int64_t segs_per_tile = (g.tile_w + args.g.segw - 1) / args.g.segw;
   const int64_t nsegs = g.ntiles_x * segs_per_tile;
-  const int64_t nwork = (ty1 - ty0) * bands_per_tile * nsegs;
+  // bands from the one holding row_begin to the one holding row_end - 1
+  args.g.band_first = (g.row_begin - ty0 * g.tile_h) / args.g.band;
+  const int64_t band_last =
+      (ty1 - 1 - ty0) * bands_per_tile + (g.row_end - 1 - (ty1 - 1) * g.tile_h) / args.g.band;
+  const int64_t nwork = (band_last - args.g.band_first + 1) * nsegs;
   // One work item per block (measured fastest: short blocks let the dispatcher
   // balance the CUs and keep each XCD's concurrent row set L2-sized; a
   // persistent grid of 8 blocks/CU was 12 % slower).
@@ -433,7 +445,7 @@ extern "C" int xrs_reproject(const void* src, int src_dtype, int64_t n, int64_t 
   g.ntiles_y = (dst_h + tile_h - 1) / tile_h;
   g.src_x = src_x; g.src_y = src_y; g.tile_x0 = tile_x0; g.tile_y0 = tile_y0;
   g.tile_win = tile_win; g.win_h = win_h; g.win_w = win_w;
-  g.x_res = x_res; g.neg_y_res = -y_res; g.err_flags = err_flags; g.band = kBand; g.segw = kSegW;
+  g.x_res = x_res; g.neg_y_res = -y_res; g.err_flags = err_flags; g.band = kBand; g.segw = kSegW; g.band_first = 0;
   a.src = src; a.n = n; a.src_sn = src_sn; a.src_sy = src_sy;
   a.dst = dst; a.dst_sn = dst_sn; a.dst_sy = dst_sy; a.fill = fill;
   a.xtab = a.ytab = nullptr;
