@@ -255,8 +255,9 @@ struct RectArgs {
   double uv_delta;
   double inv_x, inv_y;         // 1 / x_scale, 1 / y_scale (claim fast paths)
   double margin;               // window floors: relative margin (inf: always exact)
-  int exact;                   // 1: the reference's exact test at every pixel (tests)
   float margin_scale;          // form margin factor (tests: >1 widens the exact-test band)
+  int narrow;                  // dst_h * dst_w < 2^30, dst_w < 2^24: claims use 32-bit byte
+                               // offsets and 24-bit multiplies
   uint32_t* keys;              // (dst_h, dst_w) claim keys, 0xFFFFFFFF = free
   double* ij;                  // (2, dst_h, dst_w) output
 };
@@ -335,7 +336,9 @@ constexpr double kMargin = 1e-9;
 // floors of the four corners' pixel coordinates (rectify.py:500-526); floor is
 // monotone, so the window comes from the extreme corners: two floors per axis,
 // taken by the reciprocal when clearly (relative margin) away from an integer,
-// else from the reference's per-corner divisions.
+// else from the reference's per-corner divisions.  The lane then walks only
+// the pixels whose centres can be hit (trim_window: about half the window's
+// area; the cut-off pixels are misses of both triangles).
 //
 // Tests.  Per triangle (A = p0 p1 p2, B = p3 p2 p1) the reference computes
 // nu = _fu(...), nv = _fv(...) (rectify.py:737-768), u = nu / det, v = nv /
@@ -349,9 +352,11 @@ constexpr double kMargin = 1e-9;
 // decided by the forms when max over the triangles of min3 is >= 0 (some
 // triangle surely hits) or < -2M (every triangle surely misses), else — a
 // pixel centre within M of a triangle edge, rare — by the reference's exact
-// float64 test (tri_exact), so every hit / miss equals the reference's.  A
+// float64 test (tri_exact), so every hit / miss equals the reference's.  Both
+// triangles are walked in one loop on packed float32 FMAs (walk_pair).  A
 // quad with a non-finite corner or a large M takes the exact test at every
-// pixel.  Hits are claimed with a global atomicMin of the quad's key.
+// pixel of its untrimmed window.  Hits are claimed with a global atomicMin of
+// the quad's key.
 //
 // Windows larger than kLaneWindow (a quad with a NaN corner spans its whole
 // tile, rectify.py:500-526) are walked by the whole wave, 64 pixels per step,
@@ -435,6 +440,76 @@ __device__ inline bool tri_exact(const Quad& q, bool tri_b, double dx, double dy
   return u >= umin && v >= umin && u + v <= uvmax;
 }
 
+// One triangle's forms for the pair walk: 1 = forms set up, 0 = no triangle
+// (_fdet NaN or 0: never hits; forms that are -inf everywhere), -1 = no usable
+// bound (the lane takes the reference's test over the untrimmed window).
+__device__ inline int tri_forms(double ex, double ey, double e1, double e2, double e3,
+                                double e4, double cx, double cy, const RectArgs& a, float X,
+                                float Y, float wn, float hn, float umin, float uvmax,
+                                TriForms& F) {
+  const double det = e3 * e1 - e2 * e4;   // _fdet from the edge factors
+  if (det != det || det == 0.0) {
+#pragma unroll
+    for (int i = 0; i < 9; ++i) F.c[i] = 0.0f;
+    F.c[0] = -INFINITY;
+    F.thr = 0.0f;
+    return 0;
+  }
+  return tri_setup(ex, ey, e1, e2, e3, e4, det, (float)a.x_scale, (float)a.y_scale, X, Y,
+                   fabsf((float)cx), fabsf((float)cy), wn, hn, umin, uvmax, a.margin_scale, F)
+             ? 1 : -1;
+}
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+__device__ inline f32x2 form2(const TriForms& A, const TriForms& B, int i, f32x2 av, f32x2 bv) {
+  const f32x2 c0 = {A.c[i], B.c[i]}, ci = {A.c[i + 1], B.c[i + 1]}, cj = {A.c[i + 2], B.c[i + 2]};
+  return __builtin_elementwise_fma(bv, cj, __builtin_elementwise_fma(av, ci, c0));
+}
+
+// Walk the window's n pixels (row-major, nw per row) for both triangles at
+// once: triangle A in the low and B in the high half of packed float32 FMAs
+// (v_pk_fma_f32).  Returns (hit, undecided) bit masks: hit when some
+// triangle's min3 >= 0, undecided when neither hits and some min3 >= -2M.
+__device__ inline uint2 walk_pair(const TriForms& A, const TriForms& B, int n, int nw) {
+  uint32_t h_hit = 0, h_uns = 0;
+  float af = 0.0f, bf = 0.0f;
+  int col = 0;
+  for (int k = 0; k < n; ++k) {
+    const f32x2 av = {af, af}, bv = {bf, bf};
+    const f32x2 u = form2(A, B, 0, av, bv), v = form2(A, B, 3, av, bv), w = form2(A, B, 6, av, bv);
+    const float ha = fminf(u.x, fminf(v.x, w.x)), hb = fminf(u.y, fminf(v.y, w.y));
+    const uint32_t bit = 1u << k;
+    h_hit |= fmaxf(ha, hb) >= 0.0f ? bit : 0u;
+    h_uns |= (ha >= A.thr || hb >= B.thr) ? bit : 0u;
+    af += 1.0f;
+    if (++col == nw) { col = 0; af = 0.0f; bf += 1.0f; }
+  }
+  return uint2{h_hit, h_uns};
+}
+
+// Trim a quad's window [i0, i1] x [j0, j1] (floors of the corners' extreme
+// pixel units q, rectify.py:500-526) to the pixels whose centre i + 0.5 lies
+// within `pad` of [qx0, qx1] x [qy0, qy1].  A point the reference counts as a
+// hit has u, v >= -d, u + v <= 1 + 2d with d = |uv_delta| + its rounding
+// (<= the form bound M <= kMaxFormMargin, checked by tri_setup for both
+// triangles before a trimmed window is used); such points lie within
+// 4 d (extent) of the triangle's bounding box, so pad = 8 d (W + H) plus an
+// absolute 1e-6 (the rounding of q itself) leaves a factor 2 to spare.
+// Pixels cut off are misses of both triangles.
+__device__ inline void trim_window(double qx0, double qx1, double qy0, double qy1, double d,
+                                   int32_t& i0, int32_t& i1, int32_t& j0, int32_t& j1) {
+  const double pad = 8.0 * d * ((qx1 - qx0) + (qy1 - qy0)) +
+                     1e-6 * (1.0 + fmax(fmax(fabs(qx0), fabs(qx1)), fmax(fabs(qy0), fabs(qy1))));
+  const double ci = ceil(qx0 - 0.5 - pad), fi = floor(qx1 - 0.5 + pad);
+  const double cj = ceil(qy0 - 0.5 - pad), fj = floor(qy1 - 0.5 + pad);
+  const int32_t a0 = i0, a1 = i1, b0 = j0, b1 = j1;
+  if (ci > a0) i0 = (int32_t)fmin(ci, (double)a1 + 1.0);
+  if (fi < a1) i1 = (int32_t)fmax(fi, (double)a0 - 1.0);
+  if (cj > b0) j0 = (int32_t)fmin(cj, (double)b1 + 1.0);
+  if (fj < b1) j1 = (int32_t)fmax(fj, (double)b0 - 1.0);
+}
+
 __device__ inline double dpp_next_f64(double v) {   // lane i <- lane i + 1 (lane 63: 0)
   const uint64_t b = __double_as_longlong(v);
   const uint32_t lo = __builtin_amdgcn_mov_dpp((int)(uint32_t)b, 0x130, 0xF, 0xF, true);
@@ -477,7 +552,6 @@ __device__ inline Quad load_quad32(const RectArgs& a, int32_t qj, int32_t qi) {
   return load_quad(a, qj, qi);
 }
 
-__device__ inline float min3f(float x, float y, float z) { return fminf(x, fminf(y, z)); }
 
 // A quad the fast path cannot take (a non-finite corner, a pixel-unit extreme
 // close to an integer, a degenerate quad, the test knob): the reference's
@@ -590,56 +664,44 @@ rectify_claim_kernel(RectArgs a) {
           if (!(i1 < 0 || j1 < 0 || i0 >= ti.tw || j0 >= ti.th)) {
             i0 = max(i0, 0); j0 = max(j0, 0);
             i1 = min(i1, ti.tw - 1); j1 = min(j1, ti.th - 1);
-            imin = i0; jmin = j0;
-            nw = i1 - i0 + 1;
-            const int32_t nh = j1 - j0 + 1;
-            const int64_t cnt = (int64_t)nw * nh;
-            if (cnt > kLaneWindow) {
-              big_cnt = cnt;   // (a quad without a triangle is dropped there)
+            const int64_t cnt_full = (int64_t)(i1 - i0 + 1) * (j1 - j0 + 1);
+            // pixel centres (i + 0.5) farther than `pad` from the corners'
+            // extremes are misses of both triangles (trim_window)
+            int32_t ti0 = i0, ti1 = i1, tj0 = j0, tj1 = j1;
+            trim_window(qx0, qx1, qy0, qy1, fabs(a.uv_delta) + kMaxFormMargin * a.margin_scale,
+                        ti0, ti1, tj0, tj1);
+            const int64_t cnt = (int64_t)(ti1 - ti0 + 1) * (tj1 - tj0 + 1);
+            if (ti0 > ti1 || tj0 > tj1) {
+              // no pixel centre near the quad: nothing to test
+            } else if (cnt > kLaneWindow) {
+              imin = i0; jmin = j0; nw = i1 - i0 + 1;   // untrimmed: exact test everywhere
+              big_cnt = cnt_full;   // (a quad without a triangle is dropped there)
             } else {
+              imin = ti0; jmin = tj0;
+              nw = ti1 - ti0 + 1;
+              const int32_t nh = tj1 - tj0 + 1;
               const int32_t n = (int32_t)cnt;
-              const uint32_t all = (1u << n) - 1;
-              const double dx0 = ti.x_off + ((double)i0 + 0.5) * a.x_scale;   // pixel (i0, j0)
-              const double dy0 = ti.y_off + ((double)j0 + 0.5) * a.y_scale;
+              const double dx0 = ti.x_off + ((double)imin + 0.5) * a.x_scale;   // pixel (imin, jmin)
+              const double dy0 = ti.y_off + ((double)jmin + 0.5) * a.y_scale;
               const float X = fabsf((float)ti.x_off) + (float)(ti.tw + 1) * fabsf((float)a.x_scale);
               const float Y = fabsf((float)ti.y_off) + (float)(ti.th + 1) * fabsf((float)a.y_scale);
               const float wn = (float)(nw - 1), hn = (float)(nh - 1);
-              // one triangle at a time (its forms only are live during its walk)
-              auto walk = [&](double ex, double ey, double e1, double e2, double e3, double e4,
-                              double cx, double cy) -> uint2 {   // (hit, undecided) masks
-                // _fdet of the triangle from its edge factors (NaN -> 0: never hit)
-                const double det = e3 * e1 - e2 * e4;
-                if (det != det || det == 0.0) return uint2{0u, 0u};
-                TriForms F;
-                if (a.exact || !tri_setup(ex, ey, e1, e2, e3, e4, det, (float)a.x_scale,
-                                          (float)a.y_scale, X, Y, fabsf((float)cx),
-                                          fabsf((float)cy), wn, hn, (float)umin, (float)uvmax,
-                                          a.margin_scale, F))
-                  return uint2{0u, all};
-                uint32_t h_hit = 0, h_uns = 0;
-                float af = 0.0f, bf = 0.0f;
-                int32_t col = 0;
-                for (int32_t k = 0; k < n; ++k) {
-                  const float h = min3f(fmaf(bf, F.c[2], fmaf(af, F.c[1], F.c[0])),
-                                        fmaf(bf, F.c[5], fmaf(af, F.c[4], F.c[3])),
-                                        fmaf(bf, F.c[8], fmaf(af, F.c[7], F.c[6])));
-                  const uint32_t bit = 1u << k;
-                  h_hit |= h >= 0.0f ? bit : 0u;
-                  h_uns |= h < 0.0f && h >= F.thr ? bit : 0u;
-                  af += 1.0f;
-                  if (++col == nw) { col = 0; af = 0.0f; bf += 1.0f; }
-                }
-                return uint2{h_hit, h_uns};
-              };
               // A = (p0, p1, p2): _fu(p, p0, p2), _fv(p, p0, p1), _fdet(p0, p1, p2)
-              const uint2 ma = walk(t0.x - dx0, t0.y - dy0, t0.y - b0.y, t0.x - b0.x,
-                                    t0.x - t1.x, t0.y - t1.y, t0.x, t0.y);
               // B = (p3, p2, p1): _fu(p, p3, p1), _fv(p, p3, p2), _fdet(p3, p2, p1)
-              const uint2 mb = walk(b1.x - dx0, b1.y - dy0, b1.y - t1.y, b1.x - t1.x,
-                                    b1.x - b0.x, b1.y - b0.y, b1.x, b1.y);
-              hit = ma.x | mb.x;
-              unsure = ma.y | mb.y;
-              unsure &= ~hit;
+              TriForms FA, FB;
+              const int sa = tri_forms(t0.x - dx0, t0.y - dy0, t0.y - b0.y, t0.x - b0.x,
+                                       t0.x - t1.x, t0.y - t1.y, t0.x, t0.y, a, X, Y, wn, hn,
+                                       (float)umin, (float)uvmax, FA);
+              const int sb = tri_forms(b1.x - dx0, b1.y - dy0, b1.y - t1.y, b1.x - t1.x,
+                                       b1.x - b0.x, b1.y - b0.y, b1.x, b1.y, a, X, Y, wn, hn,
+                                       (float)umin, (float)uvmax, FB);
+              if (sa < 0 || sb < 0) {
+                slow = true;   // a triangle without a usable bound: exact, untrimmed window
+              } else if (sa | sb) {
+                const uint2 m = walk_pair(FA, FB, n, nw);
+                hit = m.x;
+                unsure = m.y & ~hit;
+              }
             }
           }
         } else {
@@ -652,6 +714,21 @@ rectify_claim_kernel(RectArgs a) {
       if (hit | unsure) {
         const float rnw = 1.0f / (float)nw;
         uint32_t* tile_keys = a.keys + (int64_t)ti.r0 * a.dst_w + ti.c0;
+        if (a.narrow) {
+          // 32-bit offsets from the wave-uniform tile base (no 64-bit address
+          // math per claim): pixel k of the window at lbase + k + dj (W - nw)
+          const uint32_t w32 = (uint32_t)a.dst_w;
+          const uint32_t lbase = (uint32_t)jmin * w32 + (uint32_t)imin;
+          const uint32_t lstride = w32 - (uint32_t)nw;
+          while (hit) {
+            const int k = __builtin_ctz(hit);
+            hit &= hit - 1;
+            const uint32_t dj = (uint32_t)(((float)k + 0.5f) * rnw);
+            const uint32_t off = lbase + (uint32_t)k + __umul24(dj, lstride);
+            atomicMin(reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(tile_keys) + (off << 2)),
+                      key);
+          }
+        }
         while (hit) {
           const int k = __builtin_ctz(hit);
           hit &= hit - 1;
@@ -969,11 +1046,11 @@ extern "C" int xrs_rectify_ij(const double* x, const double* y, int64_t h, int64
   // divisions for every decision
   const bool exact = xrs_testing_value(XRS_TESTING_RECTIFY_EXACT) != 0;
   a.margin = exact ? INFINITY : kMargin;
-  a.exact = exact ? 1 : 0;
   // tests: xrs_testing_set(XRS_TESTING_RECTIFY_MARGIN, k) widens the form
   // margin k-fold (more pixels take the exact test; same decisions)
   const int64_t widen = xrs_testing_value(XRS_TESTING_RECTIFY_MARGIN);
   a.margin_scale = widen > 1 ? (float)widen : 1.0f;
+  a.narrow = (dst_h * dst_w < ((int64_t)1 << 30) && dst_w < ((int64_t)1 << 24)) ? 1 : 0;
   hipStream_t st = static_cast<hipStream_t>(stream);
   XRS_HIP_CHECK(hipMemsetAsync(keys, 0xFF, (size_t)(dst_h * dst_w) * sizeof(uint32_t), st));
   {
