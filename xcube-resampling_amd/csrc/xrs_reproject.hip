@@ -134,14 +134,19 @@ __device__ inline AxisEntry resolve_axis(double coord, float origin, double res,
 // ---- K1a: axis tables ------------------------------------------------------
 template <int INTERP>
 __global__ void __launch_bounds__(kThreads)
-axis_tables_kernel(Geometry g, AxisEntry* __restrict__ xtab, AxisEntry* __restrict__ ytab) {
-  const int64_t ntiles = g.ntiles_x * g.ntiles_y;
+axis_tables_kernel(Geometry g, int64_t ty0, int64_t ty1, AxisEntry* __restrict__ xtab,
+                   AxisEntry* __restrict__ ytab) {
+  // only the tile rows [ty0, ty1) holding [row_begin, row_end) are resolved:
+  // the gathers read no other entries (a rank's row band pays for its band)
+  const int64_t t0 = ty0 * g.ntiles_x, ntiles = (ty1 - ty0) * g.ntiles_x;
   const int64_t nx = ntiles * g.tile_w, total = nx + ntiles * g.tile_h;
+  xtab += t0 * g.tile_w;
+  ytab += t0 * g.tile_h;
   int32_t eflags = 0;
   for (int64_t idx = (int64_t)blockIdx.x * kThreads + threadIdx.x; idx < total;
        idx += (int64_t)gridDim.x * kThreads) {
     if (idx < nx) {
-      const int64_t t = idx / g.tile_w, k = idx - t * g.tile_w;
+      const int64_t tl = idx / g.tile_w, k = idx - tl * g.tile_w, t = t0 + tl;
       const int64_t c = (t % g.ntiles_x) * g.tile_w + k;
       const int64_t r0 = (t / g.ntiles_x) * g.tile_h;
       AxisEntry e{-1, -1, 0.0};
@@ -152,7 +157,7 @@ axis_tables_kernel(Geometry g, AxisEntry* __restrict__ xtab, AxisEntry* __restri
       xtab[idx] = e;
     } else {
       const int64_t j = idx - nx;
-      const int64_t t = j / g.tile_h, k = j - t * g.tile_h;
+      const int64_t tl = j / g.tile_h, k = j - tl * g.tile_h, t = t0 + tl;
       const int64_t r = (t / g.ntiles_x) * g.tile_h + k;
       AxisEntry e{-1, -1, 0.0};
       if (r >= g.row_begin && r < g.row_end)
@@ -369,10 +374,10 @@ int launch(const GatherArgs& a, int coord_mode, AxisEntry* xtab, AxisEntry* ytab
   const int64_t bpc = xrs_testing_value(XRS_TESTING_REPROJECT_BLOCKS_PER_CU);
   const int nb = grid_blocks(nwork, 1, bpc > 0 ? (int)(256 * bpc) : (1 << 24));
   if (coord_mode == 0) {
-    const int64_t ntab = g.ntiles_x * g.ntiles_y * (g.tile_w + g.tile_h);
+    const int64_t ntab = g.ntiles_x * (ty1 - ty0) * (g.tile_w + g.tile_h);
     const int nbt = grid_blocks(ntab, kThreads, 256 * 8);
     hipLaunchKernelGGL((axis_tables_kernel<INTERP>), dim3(nbt), dim3(kThreads), 0, stream, g,
-                       xtab, ytab);
+                       ty0, ty1, xtab, ytab);
     XRS_HIP_CHECK(hipGetLastError());
     args.xtab = xtab;
     args.ytab = ytab;
