@@ -24,9 +24,30 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0
 
 
-def _timed(fn, steps, warmup):
+def _timed(fn, steps, warmup, graph=False):
+    """(event ms/step, wall ms/step); graph=True replays one captured call
+    (no Python/ctypes launch overhead between steps, as bench.py)."""
     import torch
 
+    if graph:   # the K timed steps captured back to back in one graph
+        fn()
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for _ in range(steps):
+                fn()
+        for _ in range(max(1, warmup)):
+            g.replay()
+        torch.cuda.synchronize()
+        stream = torch.cuda.current_stream()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        e0.record(stream)
+        g.replay()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        wall = (time.perf_counter() - t0) / steps * 1e3
+        return e0.elapsed_time(e1) / steps, wall
     for _ in range(warmup):
         fn()
     torch.cuda.synchronize()
@@ -107,7 +128,7 @@ def config1(args):
     ref = affine_ref.resample_array(a, m, (1, n, n), (1, tgm.tile_height, tgm.tile_width), 0,
                                     "first", False, np.nan)
     assert np.array_equal(out.cpu().numpy(), ref, equal_nan=True), "config 1 parity"
-    ms, wall = _timed(lambda: kernels.affine(src, plan, out), args.steps, args.warmup)
+    ms, wall = _timed(lambda: kernels.affine(src, plan, out), args.steps, args.warmup, graph=True)
     s_read = n * n  # every source pixel is read at most once (scale < 1)
     cpu_v, px, dt, cores = _cpu_pool(lambda: affine_ref.resample_array(
         a, m, (1, n, n), (1, n, n), 0, "first", False, np.nan).size, args.cpu_seconds)
@@ -132,8 +153,9 @@ def config2(args):
     src = torch.rand((1, size, size), device="cuda", dtype=torch.float32)
     out = torch.empty((1, size, size), device="cuda", dtype=torch.float64)
     flags = kernels.ErrorFlags(src.device)
-    ms, wall = _timed(lambda: kernels.reproject(src, plan, "bilinear", float("nan"),
-                                                out=out, flags=flags), args.steps, args.warmup)
+    ms, wall = _timed(lambda: kernels.reproject(src, plan, "bilinear", float("nan"), out=out,
+                                                flags=flags, check=False),
+                      args.steps, args.warmup, graph=True)
     flags.raise_if_set("config 2")
     s_read = bench.source_pixels_read(plan)
     cpu = bench.cpu_baseline(plan, tgm, args.cpu_seconds)
@@ -232,7 +254,7 @@ def config3(args):
                                     False, np.nan)
     assert np.array_equal(out[:, :c // k - 1, :c // k - 1].cpu().numpy(),
                           ref[:, :-1, :-1]), "config 3 parity"
-    ms, wall = _timed(lambda: kernels.affine(src, plan, out), args.steps, args.warmup)
+    ms, wall = _timed(lambda: kernels.affine(src, plan, out), args.steps, args.warmup, graph=True)
     cs = 2048
     sample = src[:, :cs, :cs].cpu().numpy()
     cpu_v, px, dt, cores = _cpu_pool(lambda: affine_ref.resample_array(

@@ -75,9 +75,16 @@ __device__ inline int64_t mirror(int64_t idx, int64_t n) {
   return idx;
 }
 
+// o / chunk: a 32-bit division while both fit (the usual case; a 64-bit
+// division is a long software sequence on the critical path of K2)
+__device__ inline int64_t chunk_of(int64_t o, int64_t chunk) {
+  if (((uint64_t)o | (uint64_t)chunk) <= 0x7FFFFFFFull) return (int64_t)((uint32_t)o / (uint32_t)chunk);
+  return o / chunk;
+}
+
 template <int ORDER>
 __device__ inline AxisTab axis_entry(const AxisChunks& a, int64_t o) {
-  const int64_t k = o / a.chunk, ol = o - k * a.chunk;
+  const int64_t k = chunk_of(o, a.chunk), ol = o - k * a.chunk;
   const int64_t n = a.len[k];
   const double c = a.off[k] + (double)ol * a.scale;
   AxisTab e{-1, -1, 0.0, 0.0};
@@ -113,7 +120,8 @@ __global__ void __launch_bounds__(kThreads)
 affine_tables_kernel(AxisChunks ay, AxisChunks ax, AxisTab* __restrict__ ytab,
                      AxisTab* __restrict__ xtab, int64_t dy, int64_t dx,
                      int32_t* __restrict__ nonint, const int64_t* __restrict__ t_next,
-                     int64_t nt, int32_t* __restrict__ nonself) {
+                     int64_t nt, int32_t* __restrict__ nonself, int32_t* __restrict__ yrun,
+                     int32_t* __restrict__ xrun) {
   // K3i: does any slice have a zero-weight time neighbour other than itself?
   if (nonself) {
     bool other = false;
@@ -135,6 +143,14 @@ affine_tables_kernel(AxisChunks ay, AxisChunks ax, AxisTab* __restrict__ ytab,
       const int64_t d = is_y ? dy : dx, k = o % d;
       const AxisTab f = k ? axis_entry<ORDER>(ac, o - k) : e;
       broken = broken || f.g0 < 0 || !integral_entry<ORDER>(e, f.g0, (int)k);
+      if (k == 0) {   // K3i's run record of output row / column o / d
+        bool ok = integral_entry<ORDER>(e, e.g0, 0);
+        for (int64_t j = 1; j < d && ok; ++j)
+          ok = integral_entry<ORDER>(axis_entry<ORDER>(ac, o + j), e.g0, (int)j);
+        (is_y ? yrun : xrun)[o / d] = ok ? e.g0 : -1;
+      }
+    } else if (nonint && o % (is_y ? dy : dx) == 0) {
+      (is_y ? yrun : xrun)[o / (is_y ? dy : dx)] = -1;
     }
   }
   if (nonint) {   // count of broken entries (one atomic per wave)
@@ -303,15 +319,41 @@ __device__ inline void store_value(const AffineArgs& a, int64_t didx, I v) {
 __device__ inline int32_t wave_uniform(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
 // K2 (no reduction: plain affine, or coarsen first/last/center which pick ONE
-// sub-sample): one output pixel per thread, a 64x4 tile per block, lanes on
-// consecutive output columns (coalesced xtab reads, stores and — for scales
-// near 1 — source reads), the row entry wave-uniform (scalar loads).
+// sub-sample): lanes on consecutive output columns (coalesced xtab reads,
+// stores and — for scales near 1 — source reads), a 64 x (4 x kDirectRows)
+// tile per block: each wave takes kDirectRows consecutive output rows whose
+// row entries are wave-uniform (scalar) and whose taps are all requested
+// before the first is used, so a thread pays the entry -> tap -> store chain
+// once for kDirectRows pixels (config 1: one resident round of blocks).
+constexpr int kDirectRows = 4;
+
+template <typename T, typename I, int ORDER, bool RECOVER, bool HAS_T1>
+__device__ inline void direct_rows(const AffineArgs& a, const AxisChunks& ay, const Src<T>& p,
+                                   int64_t t, int64_t oj0, int64_t oi, int sj,
+                                   const AxisTab& ex) {
+  AxisTab ey[kDirectRows];
+  Taps<T> tp[kDirectRows];
+#pragma unroll
+  for (int q = 0; q < kDirectRows; ++q) {
+    ey[q] = oj0 + q < a.out_h ? axis_entry<ORDER>(ay, (oj0 + q) * a.dy + sj)
+                              : AxisTab{-1, -1, 0.0, 0.0};   // wave-uniform
+    tp[q].template load<ORDER, HAS_T1>(p, ey[q], ex);
+  }
+#pragma unroll
+  for (int q = 0; q < kDirectRows; ++q) {
+    if (oj0 + q >= a.out_h) break;
+    const I v = tp[q].template eval<I, ORDER, RECOVER, HAS_T1>(ey[q], ex, a.cval);
+    store_value<I>(a, t * a.dst_st + (oj0 + q) * a.dst_sy + oi, v);
+  }
+}
+
 template <typename T, typename I, int ORDER, bool RECOVER>
 __global__ void __launch_bounds__(kThreads)
 affine_direct_kernel(AffineArgs a, AxisChunks ay, AxisChunks ax) {
+  constexpr int64_t kItemH = kTileH * kDirectRows;
   const int tx = threadIdx.x % kTileW;
   const int ty = wave_uniform(threadIdx.x / kTileW);
-  const int64_t ntx = (a.out_w + kTileW - 1) / kTileW, nty = (a.out_h + kTileH - 1) / kTileH;
+  const int64_t ntx = (a.out_w + kTileW - 1) / kTileW, nty = (a.out_h + kItemH - 1) / kItemH;
   const int64_t nwork = ntx * nty * a.nt;
   const XcdSlice sl = xcd_slice(nwork);
   int sj = 0, si = 0;
@@ -321,21 +363,16 @@ affine_direct_kernel(AffineArgs a, AxisChunks ay, AxisChunks ax) {
     const int64_t t = w / (ntx * nty);
     const int64_t rem = w - t * ntx * nty;
     const int64_t tj = rem / ntx, ti = rem - tj * ntx;
-    const int64_t oj = tj * kTileH + ty, oi = ti * kTileW + tx;
-    if (oj >= a.out_h) continue;
+    const int64_t oj0 = tj * kItemH + ty * kDirectRows, oi = ti * kTileW + tx;
+    if (oj0 >= a.out_h || oi >= a.out_w) continue;
     const int64_t t1 = a.t_next ? a.t_next[t] : -1;
     Src<T> p;
     p.g0 = static_cast<const T*>(a.src) + t * a.src_st;
     p.g1 = t1 >= 0 ? static_cast<const T*>(a.src) + t1 * a.src_st : p.g0;
     p.sy = a.src_sy;
-    const AxisTab ey = axis_entry<ORDER>(ay, oj * a.dy + sj);   // wave-uniform
-    if (oi < a.out_w) {
-      const AxisTab ex = axis_entry<ORDER>(ax, oi * a.dx + si);
-      I v;
-      if (ORDER == 1 && t1 >= 0) v = subsample<T, I, ORDER, RECOVER, true>(p, ey, ex, a.cval);
-      else v = subsample<T, I, ORDER, RECOVER, false>(p, ey, ex, a.cval);
-      store_value<I>(a, t * a.dst_st + oj * a.dst_sy + oi, v);
-    }
+    const AxisTab ex = axis_entry<ORDER>(ax, oi * a.dx + si);
+    if (ORDER == 1 && t1 >= 0) direct_rows<T, I, ORDER, RECOVER, true>(a, ay, p, t, oj0, oi, sj, ex);
+    else direct_rows<T, I, ORDER, RECOVER, false>(a, ay, p, t, oj0, oi, sj, ex);
   }
 }
 
@@ -547,9 +584,10 @@ affine_reduce_kernel(AffineArgs a, const AxisTab* __restrict__ ytab,
 // (order 1), is appended to a list that integral_slow_kernel evaluates
 // through the exact per-sub-sample path — same result, slower.  A list
 // longer than the workspace holds hands the whole launch to the generic K3.
-// output rows per item: 16 (f32) / 8 (f64) sub-sample rows of D elements
+// output rows per item: 32 (f32) / 16 (f64) sub-sample rows of D elements (R = 8
+// at config 3: 33 rows in flight per lane, 0.247 -> 0.240 ms vs 16)
 inline constexpr int64_t int_rows(int64_t d, int64_t esz) {
-  return d >= 8 ? 1 : (16 / d) / (esz / 4) < 1 ? 1 : (16 / d) / (esz / 4);
+  return d >= 8 ? 1 : (32 / d) / (esz / 4) < 1 ? 1 : (32 / d) / (esz / 4);
 }
 template <typename T, int D> struct IntItem {
   static constexpr int R = (int)int_rows(D, sizeof(T));
@@ -566,8 +604,8 @@ __device__ inline void load_run(const T* p, T (&v)[DX]) {
 
 template <typename T, int ORDER, int D, bool TWO>
 __global__ void __launch_bounds__(kThreads)
-affine_reduce_integral_kernel(AffineArgs a, const AxisTab* __restrict__ ytab,
-                              const AxisTab* __restrict__ xtab,
+affine_reduce_integral_kernel(AffineArgs a, const int32_t* __restrict__ yrun,
+                              const int32_t* __restrict__ xrun,
                               const int32_t* __restrict__ nonint, int32_t nonint_limit,
                               const int32_t* __restrict__ nonself, int32_t* __restrict__ nslow,
                               int64_t* __restrict__ slow_list, int64_t slow_cap) {
@@ -595,25 +633,21 @@ affine_reduce_integral_kernel(AffineArgs a, const AxisTab* __restrict__ ytab,
     const T* g1 = T1 && t1 >= 0 ? static_cast<const T*>(a.src) + t1 * a.src_st : g0;
 
     // columns: the pixel's D sub-sample columns must be one contiguous run
-    // c0 .. c0+D-1 (order 1: weight 0, right tap at +1)
-    // (entries loaded together, checked without short-circuit: one round trip)
-    AxisTab ex[D];
-    const int64_t ox = active ? oi : 0;
-#pragma unroll
-    for (int si = 0; si < D; ++si) ex[si] = xtab[ox * D + si];
-    const int32_t c0 = active ? ex[0].g0 : 0;
-    bool col_fast = active;
-#pragma unroll
-    for (int si = 0; si < D; ++si) col_fast &= integral_entry<ORDER>(ex[si], c0, si);
-    // rows: lane l checks sub-sample row l of the item (wave-uniform result)
+    // c0 .. c0+D-1 (order 1: weight 0, right tap at +1) — the tables kernel's
+    // run record (first column, -1 = not a run): 4 B per lane, one round trip
+    const int32_t c0 = active ? xrun[oi] : -1;
+    const bool col_fast = c0 >= 0;
+    // rows: output rows q < nfast take the fast path — the leading rows whose
+    // run records continue the item's first run (lane q checks output row q;
+    // wave-uniform result).  The image's last output row (mirrored tap) and a
+    // short last item no longer send the whole item to the exact path.
     const int64_t oj0 = tj * R;
     const int nrows = (int)min((int64_t)R, a.out_h - oj0);
-    const AxisTab* yitem = ytab + oj0 * D;
-    const AxisTab el = yitem[min(lane, nrows * D - 1)];
-    const int32_t gf = __builtin_amdgcn_readfirstlane(el.g0);   // lane 0's: scalar row math
-    const bool rows_fast =
-        nrows == R && __all(lane >= NE || (el.g0 >= 0 && el.g0 == gf + lane &&
-                                           (ORDER == 0 || (el.w1 == 0.0 && el.g1 == el.g0 + 1))));
+    const int32_t el = yrun[oj0 + min(lane, nrows - 1)];
+    const int32_t gf = __builtin_amdgcn_readfirstlane(el);   // lane 0's: scalar row math
+    const uint64_t okm = __ballot(lane < nrows && el >= 0 && el == gf + lane * D);
+    const int nfast = __builtin_ctzll(~okm);   // leading rows (R < 64)
+    const bool rows_fast = nfast > 0;
     const bool fast = rows_fast && col_fast;
     // loads are unconditional (a branch per row would serialise them): lanes
     // off the fast path read column 0 of the same rows and ignore the values
@@ -627,11 +661,13 @@ affine_reduce_integral_kernel(AffineArgs a, const AxisTab* __restrict__ ytab,
     if (rows_fast) {   // wave-uniform
 #pragma unroll
       for (int r = 0; r < NRT; ++r) {
-        const T* row = g0 + (int64_t)(gf + r) * a.src_sy;
+        // rows past the fast prefix are clamped into the image (values unused)
+        const int32_t rr = min(gf + r, (int32_t)(a.src_h - 1));
+        const T* row = g0 + (int64_t)rr * a.src_sy;
         load_run<T, D>(row + cl, v[r]);
         if (ORDER == 1) nbv[r] = row[cnb];
         if constexpr (T1) {
-          const T* row1 = g1 + (int64_t)(gf + r) * a.src_sy;
+          const T* row1 = g1 + (int64_t)rr * a.src_sy;
           load_run<T, D>(row1 + cl, v1[r]);
           nbv1[r] = row1[cnb];
         }
@@ -655,8 +691,9 @@ affine_reduce_integral_kernel(AffineArgs a, const AxisTab* __restrict__ ytab,
       const int64_t didx = t * a.dst_st + oj * a.dst_sy + oi;
       if (!active) continue;
       const bool lean = a.agg == AGG_MEAN || a.agg == AGG_SUM;
-      bool slow = !fast;
-      if (fast && lean) {
+      const bool fq = fast && q < nfast;
+      bool slow = !fq;
+      if (fq && lean) {
         // The values' sum equals numpy's whatever their zero signs (a signed
         // zero only flips the sign of a zero partial, and the total starts at
         // +0), so the -0 -> +0 map is not needed here.  Order 1: every value
@@ -700,7 +737,7 @@ affine_reduce_integral_kernel(AffineArgs a, const AxisTab* __restrict__ ytab,
           store_any(a.dst, didx, a.dst_dtype, res, 0, false);
           continue;
         }
-      } else if (ORDER == 1 && fast) {   // zero-weight taps: right column, row below, t+1
+      } else if (ORDER == 1 && fq) {   // zero-weight taps: right column, row below, t+1
 #pragma unroll
         for (int r = q * D; r <= q * D + D; ++r) {
           slow = slow || !is_finite(nbv[r]);
@@ -836,8 +873,8 @@ int launch(const AffineArgs& a, const AxisChunks& ay, const AxisChunks& ax, Axis
   args.ytab = ytab;
   args.xtab = xtab;
   if (direct) {   // one launch: the kernel evaluates its two table entries inline
-    const int64_t ntiles =
-        ((a.out_w + kTileW - 1) / kTileW) * ((a.out_h + kTileH - 1) / kTileH) * a.nt;
+    const int64_t ntiles = ((a.out_w + kTileW - 1) / kTileW) *
+                           ((a.out_h + kTileH * kDirectRows - 1) / (kTileH * kDirectRows)) * a.nt;
     const int nb = grid_blocks(ntiles, 1, 256 * 64);
     hipLaunchKernelGGL((affine_direct_kernel<T, I, ORDER, RECOVER>), dim3(nb), dim3(kThreads), 0,
                        st, args, ay, ax);
@@ -845,9 +882,12 @@ int launch(const AffineArgs& a, const AxisChunks& ay, const AxisChunks& ax, Axis
     return XRS_OK;
   }
   const int nbt = grid_blocks(ay.n + ax.n, kThreads, 1024);
+  // K3i's run records (one int32 per output row / column) after the slow list
+  int32_t* yrun = reinterpret_cast<int32_t*>(slow_list + slow_cap);
+  int32_t* xrun = yrun + a.out_h;
   hipLaunchKernelGGL((affine_tables_kernel<ORDER>), dim3(nbt), dim3(kThreads), 0, st, ay, ax,
                      ytab, xtab, a.dy, a.dx, k3i ? nonint : nullptr, a.t_next, a.nt,
-                     t1_flag ? nonint + 1 : nullptr);
+                     t1_flag ? nonint + 1 : nullptr, yrun, xrun);
   XRS_HIP_CHECK(hipGetLastError());
   if (k3i) {
     const int64_t ntiles = ((a.out_w + kThreads - 1) / kThreads) *
@@ -859,7 +899,7 @@ int launch(const AffineArgs& a, const AxisChunks& ay, const AxisChunks& ax, Axis
     if constexpr (std::is_floating_point<T>::value && std::is_same<T, I>::value && !RECOVER) {
 #define XRS_K3I(D, TWO, SELF)                                                             \
   hipLaunchKernelGGL((affine_reduce_integral_kernel<T, ORDER, D, TWO>), dim3(nb),         \
-                     dim3(kThreads), 0, st, args, ytab, xtab, nonint, limit, SELF,       \
+                     dim3(kThreads), 0, st, args, yrun, xrun, nonint, limit, SELF,       \
                      nonint + 2, slow_list, slow_cap)
       // with time neighbours both instances launch; nonint[1] picks one
       constexpr bool O1 = ORDER == 1;
@@ -943,10 +983,12 @@ extern "C" int xrs_any_nan(const void* src, int src_dtype, int64_t n, int32_t* f
 
 extern "C" int64_t xrs_affine_workspace_size(int64_t inter_h, int64_t inter_w) {
   if (inter_h < 0 || inter_w < 0) return 0;
-  // axis tables + the K3i flags (broken entries, time neighbour, slow count)
-  // and slow-pixel list
+  // axis tables + the K3i flags (broken entries, time neighbour, slow count),
+  // slow-pixel list
+  // and K3i's run records (out_h + out_w <= inter_h + inter_w int32)
   return (inter_h + inter_w) * (int64_t)sizeof(xrs::AxisTab) + 16 +
-         xrs::slow_capacity(inter_h, inter_w) * (int64_t)sizeof(int64_t);
+         xrs::slow_capacity(inter_h, inter_w) * (int64_t)sizeof(int64_t) +
+         (inter_h + inter_w) * (int64_t)sizeof(int32_t);
 }
 
 extern "C" int xrs_affine(const void* src, int src_dtype, int64_t nt, int64_t src_h,
