@@ -500,14 +500,9 @@ struct Fold<I, false> {
 constexpr int kReduceBatch = 2;
 
 template <typename T, typename I, int ORDER, bool RECOVER>
-__global__ void __launch_bounds__(kThreads)
-affine_reduce_kernel(AffineArgs a, const AxisTab* __restrict__ ytab,
-                     const AxisTab* __restrict__ xtab, int group,
-                     const int32_t* __restrict__ nonint, int32_t nonint_limit,
-                     int64_t slow_cap) {
+__device__ inline void reduce_body(const AffineArgs& a, const AxisTab* __restrict__ ytab,
+                                   const AxisTab* __restrict__ xtab, int group) {
   constexpr int KB = kReduceBatch;
-  // K3i (launched before) did the work, unless its slow-pixel list overflowed
-  if (nonint && *nonint <= nonint_limit && nonint[2] <= slow_cap) return;
   extern __shared__ __align__(16) unsigned char smem[];
   I* buf = reinterpret_cast<I*>(smem);
   const int tx = threadIdx.x % kTileW;
@@ -564,6 +559,13 @@ affine_reduce_kernel(AffineArgs a, const AxisTab* __restrict__ ytab,
     const int64_t oj = oj0 + ty, oi = oi0 + tx;
     if (ty < rows && oi < a.out_w) fold.store(a, t * a.dst_st + oj * a.dst_sy + oi);
   }
+}
+
+template <typename T, typename I, int ORDER, bool RECOVER>
+__global__ void __launch_bounds__(kThreads)
+affine_reduce_kernel(AffineArgs a, const AxisTab* __restrict__ ytab,
+                     const AxisTab* __restrict__ xtab, int group) {
+  reduce_body<T, I, ORDER, RECOVER>(a, ytab, xtab, group);
 }
 
 // K3i: coarsen reducers when every sub-sample of a pixel sits on a source
@@ -771,18 +773,12 @@ affine_reduce_integral_kernel(AffineArgs a, const int32_t* __restrict__ yrun,
 // wave takes 64 / D^2 listed pixels, lane l evaluates sub-sample l % D^2 of
 // its pixel through Taps (scipy's sum; all loads of a wave in flight
 // together), and the pixel's first lane folds the D^2 values in numpy's order.
-// Runs only when K3i worked and its list fit (else the generic K3 redid the
-// launch).
 template <typename T, int ORDER, int D>
-__global__ void __launch_bounds__(kThreads)
-integral_slow_kernel(AffineArgs a, const AxisTab* __restrict__ ytab,
-                     const AxisTab* __restrict__ xtab, const int32_t* __restrict__ nonint,
-                     int32_t nonint_limit, const int64_t* __restrict__ slow_list,
-                     int64_t slow_cap) {
+__device__ inline void slow_body(const AffineArgs& a, const AxisTab* __restrict__ ytab,
+                                 const AxisTab* __restrict__ xtab,
+                                 const int64_t* __restrict__ slow_list, int64_t n) {
   constexpr int S = D * D;     // sub-samples per pixel
   constexpr int G = 64 / S;    // pixels per wave
-  const int64_t n = nonint[2];
-  if (nonint[0] > nonint_limit || n > slow_cap) return;
   const int lane = threadIdx.x & 63;
   const int grp = lane / S, sub = lane % S, sj = sub / D, si = sub % D;
   const int64_t nw = (int64_t)gridDim.x * (kThreads / 64);
@@ -823,6 +819,20 @@ integral_slow_kernel(AffineArgs a, const AxisTab* __restrict__ ytab,
       fold.store(a, didx);
     }
   }
+}
+
+// The launch after K3i: its slow pixels when K3i worked and its list fit,
+// else (a grid off the integral layout, or an overflowing list) the generic
+// K3 over the whole launch — one launch either way.
+template <typename T, int ORDER, int D>
+__global__ void __launch_bounds__(kThreads)
+integral_finish_kernel(AffineArgs a, const AxisTab* __restrict__ ytab,
+                       const AxisTab* __restrict__ xtab, int group,
+                       const int32_t* __restrict__ nonint, int32_t nonint_limit,
+                       const int64_t* __restrict__ slow_list, int64_t slow_cap) {
+  const int64_t n = nonint[2];
+  if (nonint[0] <= nonint_limit && n <= slow_cap) slow_body<T, ORDER, D>(a, ytab, xtab, slow_list, n);
+  else reduce_body<T, T, ORDER, false>(a, ytab, xtab, group);
 }
 
 constexpr int kReduceLdsBudget = 32 * 1024;   // intermediate band
@@ -926,24 +936,27 @@ int launch(const AffineArgs& a, const AxisChunks& ay, const AxisChunks& ax, Axis
   const int64_t nty = (a.out_h + kRedRows - 1) / kRedRows;
   const int64_t ntx = (a.out_w + kTileW - 1) / kTileW;
   const int64_t ntiles = ntx * nty * a.nt;
-  // with K3i beside it, a small grid: it only reads the flag when K3i works
   const int nb = grid_blocks(ntiles, 1, 256 * 16);
-  const int32_t* flag = k3i ? nonint : nullptr;
-  hipLaunchKernelGGL((affine_reduce_kernel<T, I, ORDER, RECOVER>), dim3(nb), dim3(kThreads),
-                     (size_t)band, st, args, ytab, xtab, (int)group, flag, limit, slow_cap);
-  XRS_HIP_CHECK(hipGetLastError());
-  if (k3i) {
+  bool launched = false;
+  if (k3i) {   // K3i's slow pixels, or the generic K3 when K3i did not work
     if constexpr (std::is_floating_point<T>::value && std::is_same<T, I>::value && !RECOVER) {
-#define XRS_K3S(D)                                                                        \
-  hipLaunchKernelGGL((integral_slow_kernel<T, ORDER, D>), dim3(1024), dim3(kThreads), 0, st, \
-                     args, ytab, xtab, nonint, limit, slow_list, slow_cap)
-      if (a.dx == 2) XRS_K3S(2);
-      else if (a.dx == 4) XRS_K3S(4);
-      else if constexpr (sizeof(T) == 4) XRS_K3S(8);
-#undef XRS_K3S
-      XRS_HIP_CHECK(hipGetLastError());
+#define XRS_K3F(D)                                                                           \
+  do {                                                                                       \
+    hipLaunchKernelGGL((integral_finish_kernel<T, ORDER, D>), dim3(nb), dim3(kThreads),      \
+                       (size_t)band, st, args, ytab, xtab, (int)group, nonint, limit,        \
+                       slow_list, slow_cap);                                                 \
+    launched = true;                                                                         \
+  } while (0)
+      if (a.dx == 2) XRS_K3F(2);
+      else if (a.dx == 4) XRS_K3F(4);
+      else if constexpr (sizeof(T) == 4) { if (a.dx == 8) XRS_K3F(8); }
+#undef XRS_K3F
     }
   }
+  if (!launched)
+    hipLaunchKernelGGL((affine_reduce_kernel<T, I, ORDER, RECOVER>), dim3(nb), dim3(kThreads),
+                       (size_t)band, st, args, ytab, xtab, (int)group);
+  XRS_HIP_CHECK(hipGetLastError());
   return XRS_OK;
 }
 
