@@ -85,24 +85,35 @@ __device__ inline int32_t next_box(const BBoxArgs& a, const double* bx, double x
 
 // Tile rows / columns whose closed interval [b[2t], b[2t+1]] contains v, for
 // interval arrays monotone in t (dir > 0: both ends non-decreasing, dir < 0:
-// non-increasing): a contiguous run found by two binary searches instead of a
-// scan over every tile (NaN -> empty).  Same inclusive compares as the scan.
+// non-increasing): a contiguous run [t0, t1] (NaN -> empty), same inclusive
+// compares as the scan.  Both ends are found by walking from an estimate
+// (tiles are evenly spaced, so it is usually exact and a walk is 1-2 LDS
+// reads) instead of two binary searches (2 x log2(n) dependent reads); the
+// walk ends at the exact boundary whatever the estimate.
+struct Axis1 {
+  double lo0, scale;   // estimate of t: (v - lo0) * scale
+};
+__device__ inline Axis1 axis_estimate(const double* b, int32_t n) {
+  const double span = b[2 * (n - 1)] - b[0];
+  return Axis1{b[0], n > 1 && span != 0.0 ? (double)(n - 1) / span : 0.0};
+}
 __device__ inline void monotone_hits(const double* b, int32_t n, double v, int dir,
-                                     int32_t& t0, int32_t& t1) {
-  int32_t lo = 0, hi = n;   // t0: first t with (dir > 0 ? b_hi >= v : b_lo <= v)
-  while (lo < hi) {
-    const int32_t m = (lo + hi) >> 1;
-    const bool ok = dir > 0 ? b[2 * m + 1] >= v : b[2 * m] <= v;
-    if (ok) hi = m; else lo = m + 1;
-  }
-  t0 = lo;
-  lo = 0; hi = n;           // t1 + 1: first t with !(dir > 0 ? b_lo <= v : b_hi >= v)
-  while (lo < hi) {
-    const int32_t m = (lo + hi) >> 1;
-    const bool ok = dir > 0 ? b[2 * m] <= v : b[2 * m + 1] >= v;
-    if (ok) lo = m + 1; else hi = m;
-  }
-  t1 = lo - 1;
+                                     const Axis1& est, int32_t& t0, int32_t& t1) {
+  if (v != v) { t0 = 1; t1 = 0; return; }
+  const double ef = fmin(fmax((v - est.lo0) * est.scale, 0.0), (double)(n - 1));
+  const int32_t e = ef == ef ? (int32_t)ef : 0;
+  // t0: first t with P(t) = (dir > 0 ? b_hi >= v : b_lo <= v), P false..true in t
+  auto p0 = [&](int32_t t) { return dir > 0 ? b[2 * t + 1] >= v : b[2 * t] <= v; };
+  int32_t t = e;
+  if (p0(t)) { while (t > 0 && p0(t - 1)) --t; }
+  else { while (t < n && !p0(t)) ++t; }
+  t0 = t;
+  // t1 + 1: first t with !Q(t), Q(t) = (dir > 0 ? b_lo <= v : b_hi >= v), Q true..false
+  auto q1 = [&](int32_t u) { return dir > 0 ? b[2 * u] <= v : b[2 * u + 1] >= v; };
+  t = e;
+  if (q1(t)) { while (t < n && q1(t)) ++t; }
+  else { while (t > 0 && !q1(t - 1)) --t; }
+  t1 = t - 1;
 }
 
 // +1 / -1 if both interval ends are monotone non-decreasing / non-increasing
@@ -147,29 +158,47 @@ ij_bboxes_kernel(BBoxArgs a, int64_t chunk) {
   const int64_t p0 = (int64_t)blockIdx.x * chunk, p1 = min(n, p0 + chunk);
   const int xdir = a.ntx > 0 ? interval_dir(bx, (int32_t)a.ntx) : 0;
   const int ydir = a.ntx > 0 ? interval_dir(by, (int32_t)a.nty) : 0;
+  const Axis1 xest = a.ntx > 0 ? axis_estimate(bx, (int32_t)a.ntx) : Axis1{0.0, 0.0};
+  const Axis1 yest = a.ntx > 0 ? axis_estimate(by, (int32_t)a.nty) : Axis1{0.0, 0.0};
+  // the next batch's coordinates are requested before this batch's search
+  // and merges (one memory round trip hidden per iteration)
+  double xn = NAN, yn = NAN;
+  // pixel index -> (row, column) in 32-bit arithmetic (h * w <= INT32_MAX,
+  // checked by the launcher; a 64-bit division is a long VALU sequence)
+  const uint32_t w32 = (uint32_t)a.w;
+  if (p0 + threadIdx.x < p1) {
+    const uint32_t idx = (uint32_t)(p0 + threadIdx.x);
+    const uint32_t j = idx / w32;
+    xn = a.x[(int64_t)j * a.sy + (idx - j * w32)];
+    yn = a.y[(int64_t)j * a.sy + (idx - j * w32)];
+  }
   // every lane of a wave iterates the same number of times (wave-uniform trip
   // count), so the wave-wide shuffles below always see all 64 lanes
   for (int64_t base = p0; base < p1; base += kThreads) {
     const int64_t idx = base + threadIdx.x;
     const bool valid = idx < p1;
-    double x = NAN, y = NAN;
+    const double x = xn, y = yn;
     int32_t i0 = 0, j0 = 0;
     if (valid) {
-      j0 = (int32_t)(idx / a.w);
-      i0 = (int32_t)(idx - (int64_t)j0 * a.w);
-      x = a.x[(int64_t)j0 * a.sy + i0];
-      y = a.y[(int64_t)j0 * a.sy + i0];
+      j0 = (int32_t)((uint32_t)idx / w32);
+      i0 = (int32_t)((uint32_t)idx - (uint32_t)j0 * w32);
+    }
+    if (idx + kThreads < p1) {
+      const uint32_t nidx = (uint32_t)(idx + kThreads);
+      const uint32_t j = nidx / w32;
+      xn = a.x[(int64_t)j * a.sy + (nidx - j * w32)];
+      yn = a.y[(int64_t)j * a.sy + (nidx - j * w32)];
     }
     int32_t tx0 = 1, tx1 = 0, ty0 = 1, ty1 = 0;
     if (valid && a.ntx > 0) {  // x_min <= x <= x_max, y_min <= y <= y_max (bboxes.py:60-69)
       if (xdir != 0) {
-        monotone_hits(bx, (int32_t)a.ntx, x, xdir, tx0, tx1);
+        monotone_hits(bx, (int32_t)a.ntx, x, xdir, xest, tx0, tx1);
       } else {
         for (int32_t t = 0; t < (int32_t)a.ntx; ++t)
           if (bx[2 * t] <= x && x <= bx[2 * t + 1]) { if (tx0 > tx1) tx0 = t; tx1 = t; }
       }
       if (ydir != 0) {
-        monotone_hits(by, (int32_t)a.nty, y, ydir, ty0, ty1);
+        monotone_hits(by, (int32_t)a.nty, y, ydir, yest, ty0, ty1);
       } else {
         for (int32_t t = 0; t < (int32_t)a.nty; ++t)
           if (by[2 * t] <= y && y <= by[2 * t + 1]) { if (ty0 > ty1) ty0 = t; ty1 = t; }
@@ -184,12 +213,16 @@ ij_bboxes_kernel(BBoxArgs a, int64_t chunk) {
       if (k == INT32_MAX) break;
       const bool mine = cur == k;
       int32_t imin, jmin, imax, jmax;
-      const int32_t jf = __builtin_amdgcn_readfirstlane(j0);
-      if (uni && __builtin_amdgcn_readlane(j0, 63) == jf) {
-        // every lane, one source row: lanes hold consecutive pixels, so the
-        // extremes are the first and the last lane's
-        imin = __builtin_amdgcn_readfirstlane(i0);
-        imax = __builtin_amdgcn_readlane(i0, 63);
+      // lanes hold consecutive pixels: when the first and the last lane
+      // contributing to box k sit in one source row, every contributing lane
+      // does, and the extremes are those two lanes' (scalar reads, no
+      // cross-lane reductions)
+      const uint64_t mm = __ballot(mine);
+      const int fl = __builtin_ctzll(mm), ll = 63 - __builtin_clzll(mm);
+      const int32_t jf = __builtin_amdgcn_readlane(j0, fl);
+      if (__builtin_amdgcn_readlane(j0, ll) == jf) {
+        imin = __builtin_amdgcn_readlane(i0, fl);
+        imax = __builtin_amdgcn_readlane(i0, ll);
         jmin = jmax = jf;
       } else {
         imin = wave_min(mine ? i0 : INT32_MAX);
