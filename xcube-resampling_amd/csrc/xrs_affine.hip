@@ -586,10 +586,12 @@ affine_reduce_kernel(AffineArgs a, const AxisTab* __restrict__ ytab,
 // (order 1), is appended to a list that integral_slow_kernel evaluates
 // through the exact per-sub-sample path — same result, slower.  A list
 // longer than the workspace holds hands the whole launch to the generic K3.
-// output rows per item: 32 (f32) / 16 (f64) sub-sample rows of D elements (R = 8
-// at config 3: 33 rows in flight per lane, 0.247 -> 0.240 ms vs 16)
+// output rows per item: 16 (f32) / 8 (f64) sub-sample rows of D elements,
+// 32 for f32 at D = 4 (R = 8 at config 3: 33 rows in flight per lane, 0.247
+// -> 0.240 ms vs R = 4; larger R elsewhere leaves loops rolled (scratch) or
+// one wave per SIMD)
 inline constexpr int64_t int_rows(int64_t d, int64_t esz) {
-  return d >= 8 ? 1 : (32 / d) / (esz / 4) < 1 ? 1 : (32 / d) / (esz / 4);
+  return d >= 8 ? 1 : (d == 4 && esz == 4) ? 8 : (16 / d) / (esz / 4) < 1 ? 1 : (16 / d) / (esz / 4);
 }
 template <typename T, int D> struct IntItem {
   static constexpr int R = (int)int_rows(D, sizeof(T));
