@@ -348,6 +348,30 @@ int xrs_transform(const double* x, const double* y, int64_t w, int64_t h, int gr
                   const XrsProjStep* steps, int nsteps, double* out_x, double* out_y,
                   void* stream);
 
+/* -------------------------------------------------------------------------
+ * xrs_reproject_proj — xrs_reproject for non-separable CRS pairs with the
+ * coordinate transformation fused: replaces reproject.py:472-496
+ * (_transform_gridpoints: every target pixel centre -> source CRS through
+ * pyproj) together with 268-335 / 499-530 (_reproject_block on the padded
+ * window), per target pixel, without 2-D coordinate tables.
+ * grid_x (dst_w,), grid_y (dst_h,): the target grid's pixel-centre axes
+ *   (device memory); point (r, c) = (grid_x[c], grid_y[r]) is transformed by
+ *   the pipeline `steps` (HOST array, as xrs_transform; the same device code,
+ *   so the result equals xrs_transform + xrs_reproject(coord_mode 1) bit for
+ *   bit).  Every other argument as xrs_reproject; no workspace.
+ * ------------------------------------------------------------------------- */
+int xrs_reproject_proj(const void* src, int src_dtype, int64_t n, int64_t src_h,
+                       int64_t src_w, int64_t src_row0, int64_t src_rows,
+                       int64_t src_sn, int64_t src_sy, void* dst, int dst_dtype,
+                       int64_t dst_h, int64_t dst_w, int64_t row_begin,
+                       int64_t row_end, int64_t dst_sn, int64_t dst_sy,
+                       int64_t tile_h, int64_t tile_w, const double* grid_x,
+                       const double* grid_y, const XrsProjStep* steps, int nsteps,
+                       const float* tile_x0, const float* tile_y0,
+                       const int64_t* tile_win, int64_t win_h, int64_t win_w,
+                       double x_res, double y_res, int interp, double fill,
+                       int32_t* err_flags, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -220,6 +220,25 @@ def config2u(args):
           {"transform_ms": round(t_ms, 4), "k1_ms": round(k_ms, 4), "covered_px": covered,
            "transform_gpts_s": round(size * size / (t_ms / 1e3) / 1e9, 2)})
 
+    # the same step with the transformation fused into the gather
+    # (xrs_reproject_proj, what reproject_dataset runs for ONE variable)
+    import dataclasses
+    fplan = dataclasses.replace(plan, fuse_transform=True, _device_cache={})
+    fout = torch.empty_like(out)
+    f_ms, f_wall = _timed(lambda: kernels.reproject(src, fplan, "bilinear", float("nan"), out=fout,
+                                                    flags=flags, check=False),
+                          args.steps, args.warmup, graph=True)
+    flags.raise_if_set("config 2u fused")
+    assert torch.equal(torch.nan_to_num(fout, nan=-7.0), torch.nan_to_num(out, nan=-7.0)), \
+        "config 2u: fused gather differs from the tables path"
+    _line("2u-fused", "reproject bilinear 8192x8192 f32 UTM 32N (EPSG:32632) -> LAEA Europe "
+                      "(EPSG:3035) 30 m, 2048^2 tiles, f64 out; transformation fused into the "
+                      "gather (xrs_reproject_proj), bit-identical to the tables path",
+          size * size, f_ms, f_wall, 8 * size * size + 4 * size * size,
+          "gather_proj_kernel<TMERC_INV, LAEA_FWD>",
+          dict(value=round(cpu_v, 2), unit="Mpixels/s", cores=1, kind="port",
+               sample="as the 2u line"), {"covered_px": covered})
+
 
 # ------------------------------------------------------------------ config 3
 def config3(args):

@@ -122,3 +122,95 @@ def test_reproject_utm_to_laea_device_tables_match_host_tables():
     b = kernels.reproject(src, host_plan, "bilinear", np.nan).cpu().numpy()
     np.testing.assert_array_equal(np.isnan(a), np.isnan(b))
     np.testing.assert_allclose(a, b, rtol=0, atol=2e-9)   # weights differ by ~1e-9 (1e-7 m / 100 m)
+
+
+@pytest.mark.parametrize("src_crs,dst_crs", [("EPSG:32632", "EPSG:3035"),
+                                             ("EPSG:3035", "EPSG:32633"),
+                                             ("EPSG:3035", "EPSG:4326")])
+@pytest.mark.parametrize("dtype,interp,out_dtype", [
+    (np.float32, "bilinear", np.float64), (np.float32, "bilinear", np.float32),
+    (np.float32, "nearest", None), (np.float64, "triangular", None),
+    (np.uint8, "nearest", None), (np.int16, "bilinear", np.float64),
+    (np.int64, "triangular", None),
+])
+def test_fused_projection_gather_equals_tables_path(src_crs, dst_crs, dtype, interp, out_dtype):
+    """xrs_reproject_proj (the transformation evaluated inside the gather,
+    reproject.py:472-496 + 268-335 per pixel) runs the same device projection
+    code as xrs_transform, so it equals xrs_transform + K1c bit for bit — for
+    every pipeline shape, dtype, interpolation, two slices and a row band."""
+    import dataclasses
+
+    import torch
+
+    import xcube_resampling_amd as xrs
+    from xcube_resampling_amd import kernels
+
+    grids = {"EPSG:32632": ((900, 700), (400000.0, 5500000.0), 100.0),
+             "EPSG:32633": ((700, 900), (300000.0, 5400000.0), 120.0),
+             "EPSG:3035": ((800, 640), (4100000.0, 2900000.0), 110.0),
+             "EPSG:4326": ((800, 600), (8.0, 46.0), 0.0012)}
+    size, xy_min, res = grids[src_crs]
+    sgm = xrs.GridMapping.regular(size, xy_min, res, src_crs, tile_size=256)
+    tsize, txy_min, tres = grids[dst_crs]
+    tgm = xrs.GridMapping.regular(tsize, txy_min, tres, dst_crs, tile_size=(256, 192))
+    tr = xrs.Transformer.from_crs(tgm.crs, sgm.crs, always_xy=True)
+    plan = xrs.plan_reproject(sgm, tgm, tr)
+    assert plan.coord_mode == 1
+    fused = dataclasses.replace(plan, fuse_transform=True, _device_cache={})
+    rng = np.random.default_rng(11)
+    a = rng.random((2, size[1], size[0])) * 200
+    a[:, 5:9, 7:30] = np.nan if np.issubdtype(dtype, np.floating) else 0
+    src = torch.from_numpy(a.astype(dtype)).cuda()
+    assert fused.fused_transform(src.device) and not plan.fused_transform(src.device)
+    for rows in (None, (37, 301)):
+        got = kernels.reproject(src, fused, interp, np.nan if out_dtype else 0, out_dtype=out_dtype,
+                                rows=rows).cpu().numpy()
+        exp = kernels.reproject(src, plan, interp, np.nan if out_dtype else 0, out_dtype=out_dtype,
+                                rows=rows).cpu().numpy()
+        assert got.dtype == exp.dtype
+        assert np.array_equal(got, exp, equal_nan=np.issubdtype(got.dtype, np.floating))
+    assert str(src.device) not in fused._device_cache   # no coordinate tables were made
+
+
+def test_reproject_dataset_fuses_when_tables_exceed_budget():
+    """reproject_dataset on a non-separable pair: with the table budget at 0
+    the projection runs inside the gather (no coordinate tables are made),
+    and the result equals the default (tables) run bit for bit."""
+    import torch
+
+    import xcube_resampling_amd as xrs
+    from xcube_resampling_amd import kernels
+
+    n = 600
+    tgm = xrs.GridMapping.regular((500, 400), (4150000.0, 2950000.0), 100.0, "EPSG:3035",
+                                  tile_size=256)
+    a = np.random.default_rng(5).random((n, n)).astype(np.float32)
+    x = 400000.0 + (np.arange(n) + 0.5) * 100.0
+    y = 5500000.0 + (np.arange(n)[::-1] + 0.5) * 100.0
+    ds = xrs.Dataset(data_vars={"v": (("y", "x"), torch.from_numpy(a).cuda()),
+                                "w": (("y", "x"), torch.from_numpy(a[::-1].copy()).cuda())},
+                     coords={"x": ("x", x), "y": ("y", y)})
+    sgm = xrs.GridMapping.from_coords(xrs.DataArray(x, "x", name="x"),
+                                      xrs.DataArray(y, "y", name="y"), "EPSG:32632")
+    calls = []
+    orig = kernels._reproject_proj
+
+    def spy(*args, **kw):
+        calls.append(1)
+        return orig(*args, **kw)
+
+    kernels._reproject_proj = spy
+    try:
+        ref = xrs.reproject_dataset(ds, tgm, source_gm=sgm, interp_methods="bilinear")
+        assert not calls
+        with xrs.set_options(reproject_table_max_bytes=0):
+            got = xrs.reproject_dataset(ds, tgm, source_gm=sgm, interp_methods="bilinear")
+        assert len(calls) == 2   # both variables through xrs_reproject_proj
+    finally:
+        kernels._reproject_proj = orig
+    for v in ("v", "w"):
+        r, g = ref[v].values, got[v].values
+        r = r.cpu().numpy() if hasattr(r, "cpu") else r
+        g = g.cpu().numpy() if hasattr(g, "cpu") else g
+        assert np.isfinite(r).mean() > 0.5
+        assert np.array_equal(r, g, equal_nan=True)

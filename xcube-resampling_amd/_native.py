@@ -104,6 +104,15 @@ _SIGNATURES = {
                                  _c_i64, _c_i64, _c_i64, _c_ptr, _c_i64, _c_int, _c_dbl, _c_ptr]),
     "xrs_transform": (_c_int, [_c_ptr, _c_ptr, _c_i64, _c_i64, _c_int, _c_ptr, _c_int, _c_ptr,
                                _c_ptr, _c_ptr]),
+    "xrs_reproject_proj": (_c_int, [
+        _c_ptr, _c_int, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64,  # src
+        _c_ptr, _c_int, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64,          # dst
+        _c_i64, _c_i64,                                                          # tile
+        _c_ptr, _c_ptr, _c_ptr, _c_int,                                          # grid axes, steps
+        _c_ptr, _c_ptr, _c_ptr, _c_i64, _c_i64,                                  # tile tables
+        _c_dbl, _c_dbl, _c_int, _c_dbl,                                          # res, interp, fill
+        _c_ptr, _c_ptr,                                                          # flags, stream
+    ]),
 }
 
 

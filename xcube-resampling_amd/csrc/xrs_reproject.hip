@@ -41,6 +41,7 @@
 #include <type_traits>
 
 #include "xrs_common.hpp"
+#include "xrs_proj.hpp"
 
 namespace xrs {
 namespace {
@@ -303,13 +304,33 @@ gather_separable_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t bands_
   }
 }
 
+// ---- one target pixel of every dim-0 slice, from its resolved entries -------
+template <typename T, typename O, int INTERP>
+__device__ inline void gather_pixel(const GatherArgs& a, int64_t r, int64_t col,
+                                    const AxisEntry& ex, const AxisEntry& ey) {
+  const T fill = Conv<T>::from_f64(a.fill);
+  for (int64_t sn = 0; sn < a.n; ++sn) {
+    const T* src = static_cast<const T*>(a.src) + sn * a.src_sn;
+    O* dst = static_cast<O*>(a.dst) + sn * a.dst_sn + (r - a.g.row_begin) * a.dst_sy;
+    auto at = [&](int32_t row, int32_t c) -> T {
+      return (row >= 0 && c >= 0) ? src[(int64_t)row * a.src_sy + c] : fill;
+    };
+    if (INTERP == XRS_INTERP_NEAREST) {
+      dst[col] = (O)at(ey.f, ex.f);
+    } else {
+      const double v = interp4<T, INTERP>(at(ey.f, ex.f), at(ey.f, ex.c), at(ey.c, ex.f),
+                                          at(ey.c, ex.c), ex.d, ey.d);
+      dst[col] = Conv<O>::from_f64(v);
+    }
+  }
+}
+
 // ---- K1c: per-pixel gather (2-D coordinate tables) --------------------------
 template <typename T, typename O, int INTERP>
 __global__ void __launch_bounds__(kThreads)
 gather_2d_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t bands_per_tile,
                  int64_t segs_per_tile, int64_t nwork) {
   const Geometry& g = a.g;
-  const T fill = Conv<T>::from_f64(a.fill);
   int32_t eflags = 0;
   for (XcdGroups sl = xcd_groups(nwork, nsegs);; sl.i += sl.step) {
     const int64_t w = sl.item();
@@ -329,66 +350,165 @@ gather_2d_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t bands_per_til
                                                   0, g.src_w, eflags);
         const AxisEntry ey = resolve_axis<INTERP>(g.src_y[p], y0, g.neg_y_res, g.win_h, wj0,
                                                   g.src_h, g.src_row0, g.src_rows, eflags);
-        for (int64_t sn = 0; sn < a.n; ++sn) {
-          const T* src = static_cast<const T*>(a.src) + sn * a.src_sn;
-          O* dst = static_cast<O*>(a.dst) + sn * a.dst_sn + (r - g.row_begin) * a.dst_sy;
-          auto at = [&](int32_t row, int32_t col) -> T {
-            return (row >= 0 && col >= 0) ? src[(int64_t)row * a.src_sy + col] : fill;
-          };
-          if (INTERP == XRS_INTERP_NEAREST) {
-            dst[it.c0 + lc] = (O)at(ey.f, ex.f);
-          } else {
-            const double v = interp4<T, INTERP>(at(ey.f, ex.f), at(ey.f, ex.c), at(ey.c, ex.f),
-                                                at(ey.c, ex.c), ex.d, ey.d);
-            dst[it.c0 + lc] = Conv<O>::from_f64(v);
-          }
-        }
+        gather_pixel<T, O, INTERP>(a, r, it.c0 + lc, ex, ey);
       }
     }
   }
   if (eflags) atomicOr(g.err_flags, eflags);
 }
 
-template <typename T, typename O, int INTERP>
-int launch(const GatherArgs& a, int coord_mode, AxisEntry* xtab, AxisEntry* ytab,
-           hipStream_t stream) {
+// ---- K1p: per-pixel gather with the projection fused (non-separable pairs) --
+// reproject.py:472-496 + 268-335 for one target pixel: its centre
+// (grid_x[c], grid_y[r]) goes through the pipeline (xrs_proj.hpp, the code
+// xrs_transform runs), then the index math and the taps of every dim-0 slice.
+// No coordinate tables: 32 B/px less HBM traffic than xrs_transform + K1c (a
+// plan reused by several variables keeps the tables; the host decides).  The
+// pipeline is the template (its registers dominate); source / output dtype
+// and interpolation are a wave-uniform switch (`mode` = dtype code x 4 +
+// variant: 0 nearest, 1 triangular, 2 bilinear -> f32, 3 bilinear -> f64).
+__device__ inline void gather_pixel_any(int mode, const GatherArgs& a, int64_t r, int64_t col,
+                                        const AxisEntry& ex, const AxisEntry& ey) {
+  const int v = mode & 3;
+  switch (mode >> 2) {
+#define XRS_GP(CODE, T)                                                              \
+  case CODE:                                                                         \
+    if (v == 0) gather_pixel<T, T, XRS_INTERP_NEAREST>(a, r, col, ex, ey);           \
+    else if (v == 1) gather_pixel<T, T, XRS_INTERP_TRIANGULAR>(a, r, col, ex, ey);   \
+    else if (v == 2) gather_pixel<T, float, XRS_INTERP_BILINEAR>(a, r, col, ex, ey); \
+    else gather_pixel<T, double, XRS_INTERP_BILINEAR>(a, r, col, ex, ey);            \
+    break;
+    XRS_GP(XRS_DTYPE_U8, uint8_t)
+    XRS_GP(XRS_DTYPE_I8, int8_t)
+    XRS_GP(XRS_DTYPE_U16, uint16_t)
+    XRS_GP(XRS_DTYPE_I16, int16_t)
+    XRS_GP(XRS_DTYPE_U32, uint32_t)
+    XRS_GP(XRS_DTYPE_I32, int32_t)
+    XRS_GP(XRS_DTYPE_I64, int64_t)
+    XRS_GP(XRS_DTYPE_F32, float)
+    XRS_GP(XRS_DTYPE_F64, double)
+#undef XRS_GP
+    default: break;
+  }
+}
+
+template <int K0, int K1>
+__global__ void __launch_bounds__(kThreads)
+gather_proj_kernel(GatherArgs a, XrsProjStep s0, XrsProjStep s1, int mode) {
+  // one target pixel per thread and step, grid-stride over the rows of the
+  // launch (lanes on consecutive columns): the loop carries almost no state
+  // beside the projection's registers (a tile-item loop cost it one wave per
+  // SIMD of occupancy)
   const Geometry& g = a.g;
-  const int64_t ty0 = g.row_begin / g.tile_h, ty1 = (g.row_end - 1) / g.tile_h + 1;
-  GatherArgs args = a;
+  const bool nearest = (mode & 3) == 0;
+  const uint32_t w32 = (uint32_t)g.dst_w, th = (uint32_t)g.tile_h, tw = (uint32_t)g.tile_w;
+  const uint32_t ntx = (uint32_t)g.ntiles_x;
+  const int64_t p0 = g.row_begin * g.dst_w, np = (g.row_end - g.row_begin) * g.dst_w;
+  int32_t eflags = 0;
+  for (int64_t q = (int64_t)blockIdx.x * kThreads + threadIdx.x; q < np;
+       q += (int64_t)gridDim.x * kThreads) {
+    const int64_t p = p0 + q;
+    const uint32_t r = (uint32_t)(p / g.dst_w), c = (uint32_t)(p - (int64_t)r * w32);
+    const uint32_t t = (r / th) * ntx + c / tw;
+    double px = g.src_x[c], py = g.src_y[r];   // the target pixel centre
+    if constexpr (K0 != 0) proj::apply_step<K0>(s0, px, py);
+    if constexpr (K1 != 0) proj::apply_step<K1>(s1, px, py);
+    const float x0 = g.tile_x0[t], y0 = g.tile_y0[t];
+    const int64_t wi0 = g.tile_win[2 * t], wj0 = g.tile_win[2 * t + 1];
+    AxisEntry ex, ey;
+    if (nearest) {
+      ex = resolve_axis<XRS_INTERP_NEAREST>(px, x0, g.x_res, g.win_w, wi0, g.src_w, 0, g.src_w,
+                                            eflags);
+      ey = resolve_axis<XRS_INTERP_NEAREST>(py, y0, g.neg_y_res, g.win_h, wj0, g.src_h,
+                                            g.src_row0, g.src_rows, eflags);
+    } else {
+      ex = resolve_axis<XRS_INTERP_BILINEAR>(px, x0, g.x_res, g.win_w, wi0, g.src_w, 0, g.src_w,
+                                             eflags);
+      ey = resolve_axis<XRS_INTERP_BILINEAR>(py, y0, g.neg_y_res, g.win_h, wj0, g.src_h,
+                                             g.src_row0, g.src_rows, eflags);
+    }
+    gather_pixel_any(mode, a, r, c, ex, ey);
+  }
+  if (eflags) atomicOr(g.err_flags, eflags);
+}
+
+// Work decomposition of the gathers (K1b/K1c/K1p): bands from the one holding
+// row_begin to the one holding row_end - 1, all segments of a band together.
+struct Work {
+  GatherArgs args;
+  int64_t ty0, ty1, nsegs, bands_per_tile, segs_per_tile, nwork;
+  int nb;
+};
+inline Work work_of(const GatherArgs& a) {
+  const Geometry& g = a.g;
+  Work k;
+  k.args = a;
+  k.ty0 = g.row_begin / g.tile_h;
+  k.ty1 = (g.row_end - 1) / g.tile_h + 1;
   // band height / grid cap: fixed in the product; xrs_testing_set() can change
   // them so the tests cover items that split tiles and the grid-stride loop
   const int64_t band_knob = xrs_testing_value(XRS_TESTING_REPROJECT_BAND);
-  args.g.band = band_knob > 0 ? band_knob : kBand;
-  args.g.segw = kSegW;
-  const int64_t bands_per_tile = (g.tile_h + args.g.band - 1) / args.g.band;
-  const int64_t segs_per_tile = (g.tile_w + args.g.segw - 1) / args.g.segw;
-  const int64_t nsegs = g.ntiles_x * segs_per_tile;
-  // bands from the one holding row_begin to the one holding row_end - 1
-  args.g.band_first = (g.row_begin - ty0 * g.tile_h) / args.g.band;
-  const int64_t band_last =
-      (ty1 - 1 - ty0) * bands_per_tile + (g.row_end - 1 - (ty1 - 1) * g.tile_h) / args.g.band;
-  const int64_t nwork = (band_last - args.g.band_first + 1) * nsegs;
+  k.args.g.band = band_knob > 0 ? band_knob : kBand;
+  k.args.g.segw = kSegW;
+  k.bands_per_tile = (g.tile_h + k.args.g.band - 1) / k.args.g.band;
+  k.segs_per_tile = (g.tile_w + k.args.g.segw - 1) / k.args.g.segw;
+  k.nsegs = g.ntiles_x * k.segs_per_tile;
+  k.args.g.band_first = (g.row_begin - k.ty0 * g.tile_h) / k.args.g.band;
+  const int64_t band_last = (k.ty1 - 1 - k.ty0) * k.bands_per_tile +
+                            (g.row_end - 1 - (k.ty1 - 1) * g.tile_h) / k.args.g.band;
+  k.nwork = (band_last - k.args.g.band_first + 1) * k.nsegs;
   // One work item per block (measured fastest: short blocks let the dispatcher
   // balance the CUs and keep each XCD's concurrent row set L2-sized; a
   // persistent grid of 8 blocks/CU was 12 % slower).
   const int64_t bpc = xrs_testing_value(XRS_TESTING_REPROJECT_BLOCKS_PER_CU);
-  const int nb = grid_blocks(nwork, 1, bpc > 0 ? (int)(256 * bpc) : (1 << 24));
+  k.nb = grid_blocks(k.nwork, 1, bpc > 0 ? (int)(256 * bpc) : (1 << 24));
+  return k;
+}
+
+template <typename T, typename O, int INTERP>
+int launch(const GatherArgs& a, int coord_mode, AxisEntry* xtab, AxisEntry* ytab,
+           hipStream_t stream) {
+  const Geometry& g = a.g;
+  Work k = work_of(a);
   if (coord_mode == 0) {
-    const int64_t ntab = g.ntiles_x * (ty1 - ty0) * (g.tile_w + g.tile_h);
+    const int64_t ntab = g.ntiles_x * (k.ty1 - k.ty0) * (g.tile_w + g.tile_h);
     const int nbt = grid_blocks(ntab, kThreads, 256 * 8);
     hipLaunchKernelGGL((axis_tables_kernel<INTERP>), dim3(nbt), dim3(kThreads), 0, stream, g,
-                       ty0, ty1, xtab, ytab);
+                       k.ty0, k.ty1, xtab, ytab);
     XRS_HIP_CHECK(hipGetLastError());
-    args.xtab = xtab;
-    args.ytab = ytab;
-    hipLaunchKernelGGL((gather_separable_kernel<T, O, INTERP>), dim3(nb), dim3(kThreads), 0,
-                       stream, args, ty0, nsegs, bands_per_tile, segs_per_tile, nwork);
+    k.args.xtab = xtab;
+    k.args.ytab = ytab;
+    hipLaunchKernelGGL((gather_separable_kernel<T, O, INTERP>), dim3(k.nb), dim3(kThreads), 0,
+                       stream, k.args, k.ty0, k.nsegs, k.bands_per_tile, k.segs_per_tile, k.nwork);
   } else {
-    hipLaunchKernelGGL((gather_2d_kernel<T, O, INTERP>), dim3(nb), dim3(kThreads), 0, stream,
-                       args, ty0, nsegs, bands_per_tile, segs_per_tile, nwork);
+    hipLaunchKernelGGL((gather_2d_kernel<T, O, INTERP>), dim3(k.nb), dim3(kThreads), 0, stream,
+                       k.args, k.ty0, k.nsegs, k.bands_per_tile, k.segs_per_tile, k.nwork);
   }
   XRS_HIP_CHECK(hipGetLastError());
   return XRS_OK;
+}
+
+template <int K0, int K1>
+int launch_proj(const GatherArgs& a, const XrsProjStep& s0, const XrsProjStep& s1, int mode,
+                hipStream_t stream) {
+  const int64_t np = (a.g.row_end - a.g.row_begin) * a.g.dst_w;
+  const int nb = grid_blocks(np, kThreads, 256 * 16);
+  hipLaunchKernelGGL((gather_proj_kernel<K0, K1>), dim3(nb), dim3(kThreads), 0, stream, a, s0,
+                     s1, mode);
+  XRS_HIP_CHECK(hipGetLastError());
+  return XRS_OK;
+}
+
+// pipelines of crs.Transformer: [inverse], [forward], [inverse, forward]
+template <int K0>
+int launch_proj_second(int k1, const GatherArgs& a, const XrsProjStep& s0,
+                       const XrsProjStep& s1, int mode, hipStream_t st) {
+  switch (k1) {
+    case 0: return launch_proj<K0, 0>(a, s0, s1, mode, st);
+    case XRS_PROJ_WEBMERC_FWD: return launch_proj<K0, XRS_PROJ_WEBMERC_FWD>(a, s0, s1, mode, st);
+    case XRS_PROJ_TMERC_FWD: return launch_proj<K0, XRS_PROJ_TMERC_FWD>(a, s0, s1, mode, st);
+    case XRS_PROJ_LAEA_FWD: return launch_proj<K0, XRS_PROJ_LAEA_FWD>(a, s0, s1, mode, st);
+    default: return XRS_ERR_ARG;
+  }
 }
 
 }  // namespace
@@ -468,4 +588,90 @@ extern "C" int xrs_reproject(const void* src, int src_dtype, int64_t n, int64_t 
       return launch<T, float, XRS_INTERP_BILINEAR>(a, coord_mode, xtab, ytab, st);
     return launch<T, double, XRS_INTERP_BILINEAR>(a, coord_mode, xtab, ytab, st);
   });
+}
+
+extern "C" int xrs_reproject_proj(const void* src, int src_dtype, int64_t n, int64_t src_h,
+                                  int64_t src_w, int64_t src_row0, int64_t src_rows,
+                                  int64_t src_sn, int64_t src_sy, void* dst, int dst_dtype,
+                                  int64_t dst_h, int64_t dst_w, int64_t row_begin,
+                                  int64_t row_end, int64_t dst_sn, int64_t dst_sy,
+                                  int64_t tile_h, int64_t tile_w, const double* grid_x,
+                                  const double* grid_y, const XrsProjStep* steps, int nsteps,
+                                  const float* tile_x0, const float* tile_y0,
+                                  const int64_t* tile_win, int64_t win_h, int64_t win_w,
+                                  double x_res, double y_res, int interp, double fill,
+                                  int32_t* err_flags, void* stream) {
+  using namespace xrs;
+  if (interp != XRS_INTERP_NEAREST && interp != XRS_INTERP_BILINEAR &&
+      interp != XRS_INTERP_TRIANGULAR) {
+    xrs_set_error("interp must be nearest(0), bilinear(1) or triangular(2), was %d", interp);
+    return XRS_ERR_NOTIMPL;
+  }
+  if (!src || !dst || !grid_x || !grid_y || !tile_x0 || !tile_y0 || !tile_win || !err_flags ||
+      n < 1 || src_h < 1 || src_w < 1 || dst_h < 1 || dst_w < 1 || tile_h < 1 || tile_w < 1 ||
+      win_h < 1 || win_w < 1 || row_begin < 0 || row_end > dst_h || row_begin > row_end ||
+      src_rows < 0 || src_sy < src_w || src_w > INT32_MAX || src_rows > INT32_MAX ||
+      nsteps < 0 || nsteps > 2 || (nsteps > 0 && !steps) || dst_h > INT32_MAX ||
+      dst_w > INT32_MAX) {
+    xrs_set_error("xrs_reproject_proj: invalid argument");
+    return XRS_ERR_ARG;
+  }
+  const int k0 = nsteps > 0 ? steps[0].kind : 0, k1 = nsteps > 1 ? steps[1].kind : 0;
+  const bool fwd0 = k0 == XRS_PROJ_WEBMERC_FWD || k0 == XRS_PROJ_TMERC_FWD ||
+                    k0 == XRS_PROJ_LAEA_FWD;
+  if ((nsteps > 0 && (k0 < XRS_PROJ_WEBMERC_FWD || k0 > XRS_PROJ_LAEA_INV)) ||
+      (nsteps > 1 && (fwd0 || !(k1 == XRS_PROJ_WEBMERC_FWD || k1 == XRS_PROJ_TMERC_FWD ||
+                                k1 == XRS_PROJ_LAEA_FWD)))) {
+    xrs_set_error("xrs_reproject_proj: unsupported projection pipeline");
+    return XRS_ERR_ARG;
+  }
+  if (row_begin == row_end) return XRS_OK;
+  int variant;
+  if (interp == XRS_INTERP_BILINEAR) {
+    if (dst_dtype != XRS_DTYPE_F32 && dst_dtype != XRS_DTYPE_F64) {
+      xrs_set_error("xrs_reproject_proj: bilinear output dtype must be float32 or float64");
+      return XRS_ERR_ARG;
+    }
+    variant = dst_dtype == XRS_DTYPE_F32 ? 2 : 3;
+  } else {
+    if (dst_dtype != src_dtype) {
+      xrs_set_error("xrs_reproject_proj: nearest/triangular output dtype must equal the source dtype");
+      return XRS_ERR_ARG;
+    }
+    variant = interp == XRS_INTERP_NEAREST ? 0 : 1;
+  }
+  if (dispatch_dtype(src_dtype, [](auto) { return XRS_OK; }) != XRS_OK) {
+    xrs_set_error("xrs_reproject_proj: unsupported source dtype %d", src_dtype);
+    return XRS_ERR_ARG;
+  }
+  GatherArgs a;
+  Geometry& g = a.g;
+  g.src_h = src_h; g.src_w = src_w; g.src_row0 = src_row0; g.src_rows = src_rows;
+  g.dst_h = dst_h; g.dst_w = dst_w; g.row_begin = row_begin; g.row_end = row_end;
+  g.tile_h = tile_h; g.tile_w = tile_w;
+  g.ntiles_x = (dst_w + tile_w - 1) / tile_w;
+  g.ntiles_y = (dst_h + tile_h - 1) / tile_h;
+  g.src_x = grid_x; g.src_y = grid_y; g.tile_x0 = tile_x0; g.tile_y0 = tile_y0;
+  g.tile_win = tile_win; g.win_h = win_h; g.win_w = win_w;
+  g.x_res = x_res; g.neg_y_res = -y_res; g.err_flags = err_flags; g.band = kBand; g.segw = kSegW; g.band_first = 0;
+  a.src = src; a.n = n; a.src_sn = src_sn; a.src_sy = src_sy;
+  a.dst = dst; a.dst_sn = dst_sn; a.dst_sy = dst_sy; a.fill = fill;
+  a.xtab = a.ytab = nullptr;
+  XrsProjStep s0{}, s1{};
+  if (nsteps > 0) s0 = steps[0];
+  if (nsteps > 1) s1 = steps[1];
+  const int mode = src_dtype * 4 + variant;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  switch (k0) {
+    case 0: return launch_proj<0, 0>(a, s0, s1, mode, st);
+    case XRS_PROJ_WEBMERC_FWD: return launch_proj<XRS_PROJ_WEBMERC_FWD, 0>(a, s0, s1, mode, st);
+    case XRS_PROJ_TMERC_FWD: return launch_proj<XRS_PROJ_TMERC_FWD, 0>(a, s0, s1, mode, st);
+    case XRS_PROJ_LAEA_FWD: return launch_proj<XRS_PROJ_LAEA_FWD, 0>(a, s0, s1, mode, st);
+    case XRS_PROJ_WEBMERC_INV:
+      return launch_proj_second<XRS_PROJ_WEBMERC_INV>(k1, a, s0, s1, mode, st);
+    case XRS_PROJ_TMERC_INV:
+      return launch_proj_second<XRS_PROJ_TMERC_INV>(k1, a, s0, s1, mode, st);
+    default:
+      return launch_proj_second<XRS_PROJ_LAEA_INV>(k1, a, s0, s1, mode, st);
+  }
 }

@@ -7,15 +7,9 @@
 //   * rectify.py:182-231 (_transform_coords): every source coordinate ->
 //     target CRS.
 // A pipeline is one or two steps (source -> geographic -> target, crs.py
-// Transformer), each a template parameter of the kernel; each step restates one PROJ operation exactly
-// as xcube_resampling_amd/projections.py + crs.py do in numpy (same formulas,
-// same operation order, -ffp-contract=off): web Mercator (merc_s, webmerc),
-// transverse Mercator (tmerc poder_engsager: Clenshaw gatg / clenS) and
-// Lambert azimuthal equal area (laea e_forward / e_inverse), around PROJ's
-// pj_fwd / pj_inv (lam0 + adjlon, unit-ellipsoid scaling, false origin).
-// The device libm differs from the host's in the last bit of some
-// transcendentals, so results agree with the numpy restatement to a few ulps
-// (tests/test_transform_gpu.py), not bit for bit.
+// Transformer), each a template parameter of the kernel; the steps are the
+// PROJ restatements of xrs_proj.hpp (a few ulps from the numpy restatement,
+// tests/test_transform_gpu.py).
 //
 // Launch: one thread per point, grid-stride; compute bound (f64 VALU and the
 // transcendental sequences), 16 B in (image mode) and 16 B out per point.
@@ -23,234 +17,13 @@
 #include <cmath>
 
 #include "xrs_common.hpp"
+#include "xrs_proj.hpp"
 
 namespace xrs {
 namespace {
 
 constexpr int kThreads = 256;
-constexpr double kDegToRad = 0.017453292519943296;   // crs._DEG_TO_RAD
-constexpr double kPi = 3.141592653589793;
-
-// ---- PROJ helpers (projections.py) ---------------------------------------------
-// Clenshaw summation for the Gaussian <-> geodetic latitude (tmerc.cpp gatg)
-__device__ inline double gatg(const double* p, double B, double cos_2B, double sin_2B) {
-  const double two_cos_2B = 2.0 * cos_2B;
-  double h2 = 0.0, h1 = p[5], h = 0.0;
-#pragma unroll
-  for (int k = 4; k >= 0; --k) {
-    h = -h2 + two_cos_2B * h1 + p[k];
-    h2 = h1;
-    h1 = h;
-  }
-  return B + h * sin_2B;
-}
-
-// complex Clenshaw summation (tmerc.cpp clenS)
-__device__ inline void clenS(const double* a, double sin_arg_r, double cos_arg_r,
-                             double sinh_arg_i, double cosh_arg_i, double& dr, double& di) {
-  double r = 2.0 * cos_arg_r * cosh_arg_i;
-  double i = -2.0 * sin_arg_r * sinh_arg_i;
-  double hi1 = 0.0, hr1 = 0.0, hi = 0.0, hr = a[5];
-#pragma unroll
-  for (int k = 4; k >= 0; --k) {
-    const double hr2 = hr1, hi2 = hi1;
-    hr1 = hr;
-    hi1 = hi;
-    hr = -hr2 + r * hr1 - i * hi1 + a[k];
-    hi = -hi2 + i * hr1 + r * hi1;
-  }
-  r = sin_arg_r * cosh_arg_i;
-  i = cos_arg_r * sinh_arg_i;
-  dr = r * hr - i * hi;
-  di = r * hi + i * hr;
-}
-
-__device__ inline void tmerc_fwd(const XrsProjStep& s, double lam, double phi, double& x,
-                                 double& y) {
-  const double* cbg = s.c + 6;
-  const double* gtu = s.c + 18;
-  double s2p, c2p, sin_Cn, cos_Cn, sin_Ce, cos_Ce;
-  sincos(2 * phi, &s2p, &c2p);
-  double Cn = gatg(cbg, phi, c2p, s2p);
-  sincos(Cn, &sin_Cn, &cos_Cn);
-  sincos(lam, &sin_Ce, &cos_Ce);
-  const double cos_Cn_cos_Ce = cos_Cn * cos_Ce;
-  Cn = atan2(sin_Cn, cos_Cn_cos_Ce);
-  const double inv_denom_tan_Ce = 1.0 / hypot(sin_Cn, cos_Cn_cos_Ce);
-  const double tan_Ce = sin_Ce * cos_Cn * inv_denom_tan_Ce;
-  double Ce = asinh(tan_Ce);
-  const double two_inv_denom_tan_Ce = 2 * inv_denom_tan_Ce;
-  const double two_inv_denom_tan_Ce_square = two_inv_denom_tan_Ce * inv_denom_tan_Ce;
-  const double tmp_r = cos_Cn_cos_Ce * two_inv_denom_tan_Ce_square;
-  const double sin_arg_r = sin_Cn * tmp_r;
-  const double cos_arg_r = cos_Cn_cos_Ce * tmp_r - 1;
-  const double sinh_arg_i = tan_Ce * two_inv_denom_tan_Ce;
-  const double cosh_arg_i = two_inv_denom_tan_Ce_square - 1;
-  double dCn, dCe;
-  clenS(gtu, sin_arg_r, cos_arg_r, sinh_arg_i, cosh_arg_i, dCn, dCe);
-  Cn = Cn + dCn;
-  Ce = Ce + dCe;
-  const bool ok = fabs(Ce) <= 2.623395162778;
-  x = ok ? s.Qn * Ce : INFINITY;
-  y = ok ? s.Qn * Cn + s.Zb : INFINITY;
-}
-
-__device__ inline void tmerc_inv(const XrsProjStep& s, double x, double y, double& lam,
-                                 double& phi) {
-  const double* cgb = s.c;
-  const double* utg = s.c + 12;
-  double Cn = (y - s.Zb) / s.Qn;
-  double Ce = x / s.Qn;
-  const bool ok = fabs(Ce) <= 2.623395162778;
-  double sin_arg_r, cos_arg_r;
-  sincos(2 * Cn, &sin_arg_r, &cos_arg_r);
-  const double exp_2_Ce = exp(2 * Ce);
-  const double half_inv_exp_2_Ce = 0.5 / exp_2_Ce;
-  const double sinh_arg_i = 0.5 * exp_2_Ce - half_inv_exp_2_Ce;
-  const double cosh_arg_i = 0.5 * exp_2_Ce + half_inv_exp_2_Ce;
-  double dCn, dCe;
-  clenS(utg, sin_arg_r, cos_arg_r, sinh_arg_i, cosh_arg_i, dCn, dCe);
-  Cn = Cn + dCn;
-  Ce = Ce + dCe;
-  double sin_Cn, cos_Cn;
-  sincos(Cn, &sin_Cn, &cos_Cn);
-  const double sinhCe = sinh(Ce);
-  Ce = atan2(sinhCe, cos_Cn);
-  const double modulus_Ce = hypot(sinhCe, cos_Cn);
-  Cn = atan2(sin_Cn, modulus_Ce);
-  const double tmp = 2 * modulus_Ce / (sinhCe * sinhCe + 1);
-  const double sin_2_Cn = sin_Cn * tmp;
-  const double cos_2_Cn = tmp * modulus_Ce - 1.0;
-  const double ph = gatg(cgb, Cn, cos_2_Cn, sin_2_Cn);
-  lam = ok ? Ce : INFINITY;
-  phi = ok ? ph : INFINITY;
-}
-
-// laea modes (projections.py LambertAzimuthalEqualArea.mode)
-constexpr int kNPole = 0, kSPole = 1, kEquit = 2, kObliq = 3;
-constexpr double kEps10 = 1.0e-10;
-
-__device__ inline double qsfn(double sinphi, double e, double one_es) {
-  const double con = e * sinphi;
-  const double div1 = 1.0 - con * con;
-  const double div2 = 1.0 + con;
-  return one_es * (sinphi / div1 - (0.5 / e) * log((1.0 - con) / div2));
-}
-
-// np.clip(v, -1, 1) (NaN stays NaN)
-__device__ inline double clip1(double v) { return v < -1.0 ? -1.0 : (v > 1.0 ? 1.0 : v); }
-
-__device__ inline double authlat(const XrsProjStep& s, double beta) {
-  const double t = beta + beta;
-  return beta + s.apa[0] * sin(t) + s.apa[1] * sin(t + t) + s.apa[2] * sin(t + t + t);
-}
-
-__device__ inline void laea_fwd(const XrsProjStep& s, double lam, double phi, double& x,
-                                double& y) {
-  double sinlam, coslam;
-  sincos(lam, &sinlam, &coslam);
-  const double sinphi = sin(phi);
-  double q = qsfn(sinphi, s.e, s.one_es);
-  if (s.mode == kObliq || s.mode == kEquit) {
-    const double sinb = q / s.qp;
-    const double cosb2 = 1.0 - sinb * sinb;
-    const double cosb = cosb2 > 0 ? sqrt(fmax(cosb2, 0.0)) : 0.0;
-    double b = s.mode == kObliq ? 1.0 + s.sinb1 * sinb + s.cosb1 * cosb * coslam
-                                : 1.0 + cosb * coslam;
-    const bool bad = fabs(b) < kEps10;
-    b = sqrt(2.0 / (bad ? 1.0 : b));
-    const double yy = s.mode == kObliq ? s.ymf * b * (s.cosb1 * sinb - s.sinb1 * cosb * coslam)
-                                       : b * sinb * s.ymf;
-    const double xx = s.xmf * b * cosb * sinlam;
-    x = bad ? INFINITY : xx;
-    y = bad ? INFINITY : yy;
-    return;
-  }
-  q = s.mode == kNPole ? s.qp - q : s.qp + q;
-  const bool pos = q >= 1e-15;
-  const double b = sqrt(pos ? q : 0.0);
-  x = pos ? b * sinlam : 0.0;
-  y = pos ? coslam * (s.phi0 < 0.0 ? b : -b) : 0.0;
-}
-
-__device__ inline void laea_inv(const XrsProjStep& s, double x, double y, double& lam,
-                                double& phi) {
-  if (s.mode == kObliq || s.mode == kEquit) {
-    x = x / s.dd;
-    y = y * s.dd;
-    const double rho = hypot(x, y);
-    const bool small = rho < kEps10;
-    const double rho_s = small ? 1.0 : rho;
-    const double asin_arg = 0.5 * rho_s / s.rq;
-    const bool bad = asin_arg > 1.0;
-    double sCe, cCe;
-    sincos(2.0 * asin(asin_arg > 1.0 ? 1.0 : asin_arg), &sCe, &cCe);   // np.minimum keeps NaN
-    x = x * sCe;
-    double ab;
-    if (s.mode == kObliq) {
-      ab = cCe * s.sinb1 + y * sCe * s.cosb1 / rho_s;
-      y = rho_s * s.cosb1 * cCe - y * s.sinb1 * sCe;
-    } else {
-      ab = y * sCe / rho_s;
-      y = rho_s * cCe;
-    }
-    double l = atan2(x, y);
-    double p = authlat(s, asin(clip1(ab)));
-    l = small ? 0.0 : l;
-    p = small ? s.phi0 : p;
-    lam = bad ? INFINITY : l;
-    phi = bad ? INFINITY : p;
-    return;
-  }
-  if (s.mode == kNPole) y = -y;
-  const double q = x * x + y * y;
-  double ab = 1.0 - q / s.qp;
-  if (s.mode == kSPole) ab = -ab;
-  lam = atan2(x, y);
-  phi = authlat(s, asin(clip1(ab)));
-}
-
-// PROJ adjlon as crs._adjlon: wrap to [-pi, pi] when outside by more than 1e-12
-__device__ inline double adjlon(double lam) {
-  if (!(fabs(lam) >= kPi + 1e-12)) return lam;
-  double w = lam + kPi;
-  w = w - 2 * kPi * floor(w / (2 * kPi)) - kPi;
-  return w;
-}
-
-// one pipeline step (crs._projection forward / inverse, webmerc_forward /
-// _inverse); the kind is a template parameter, so a kernel holds only the code
-// (and registers) of its own pipeline
-template <int KIND>
-__device__ inline void apply_step(const XrsProjStep& s, double& x, double& y) {
-  const double rad_to_deg = 1.0 / kDegToRad;   // crs._RAD_TO_DEG_FACTOR
-  if constexpr (KIND == XRS_PROJ_WEBMERC_FWD) {
-    const double lam = x * kDegToRad, phi = y * kDegToRad;
-    x = s.a * lam;
-    y = s.a * asinh(tan(phi));
-  } else if constexpr (KIND == XRS_PROJ_WEBMERC_INV) {
-    const double lam = x * s.ra;
-    const double phi = atan(sinh(y * s.ra));
-    x = lam * rad_to_deg;
-    y = phi * rad_to_deg;
-  } else if constexpr (KIND == XRS_PROJ_TMERC_FWD || KIND == XRS_PROJ_LAEA_FWD) {
-    const double lam = adjlon(x * kDegToRad - s.lam0);
-    const double phi = y * kDegToRad;
-    double px, py;
-    if constexpr (KIND == XRS_PROJ_TMERC_FWD) tmerc_fwd(s, lam, phi, px, py);
-    else laea_fwd(s, lam, phi, px, py);
-    x = s.a * px + s.x0;
-    y = s.a * py + s.y0;
-  } else if constexpr (KIND == XRS_PROJ_TMERC_INV || KIND == XRS_PROJ_LAEA_INV) {
-    const double xx = (x - s.x0) * s.ra, yy = (y - s.y0) * s.ra;
-    double lam, phi;
-    if constexpr (KIND == XRS_PROJ_TMERC_INV) tmerc_inv(s, xx, yy, lam, phi);
-    else laea_inv(s, xx, yy, lam, phi);
-    lam = adjlon(lam + s.lam0);
-    x = lam * rad_to_deg;
-    y = phi * rad_to_deg;
-  }
-}
+using proj::apply_step;
 
 // grid mode: point (r, c) = (x[c], y[r]) (a regular grid's pixel centres,
 // np.meshgrid order); image mode: point p = (x[p], y[p]).  Out row-major.

@@ -74,6 +74,9 @@ def reproject(src, plan, interp: str, fill: float, out_dtype=None, rows=None, ou
         src = torch().zeros((n, 1, w), dtype=src.dtype, device=device)
     if out is None:
         out = empty((n, r1 - r0, plan.dst_width), out_dtype, device)
+    if plan.fused_transform(device):
+        return _reproject_proj(src, plan, interp_code, fill, out_dtype, r0, r1, out, src_row0,
+                               flags, check, stream)
     tables = plan.device_tables(device)
     lib = _native.lib()
     ws_bytes = lib.xrs_reproject_workspace_size(plan.dst_height, plan.dst_width, plan.tile_height,
@@ -96,6 +99,34 @@ def reproject(src, plan, interp: str, fill: float, out_dtype=None, rows=None, ou
         interp_code, float(fill), ptr(ws) if ws is not None else None, ws_bytes, flags.ptr,
         stream_handle(device, stream))
     _native.check(rc, "xrs_reproject")
+    if own_flags and check:
+        flags.raise_if_set("reproject")
+    return out
+
+
+def _reproject_proj(src, plan, interp_code, fill, out_dtype, r0, r1, out, src_row0, flags,
+                    check, stream):
+    """xrs_reproject_proj: the non-separable plan's transformation fused into
+    the gather (reproject.py:472-496 + 268-335 per target pixel, no 2-D
+    coordinate tables)."""
+    device = src.device
+    n, h_band, _ = src.shape
+    tabs = plan.device_grid(device)
+    steps, nsteps = plan.transformer.device_steps()
+    own_flags = flags is None
+    if own_flags:
+        flags = ErrorFlags(device)
+    sn, sy, _ = src.stride()
+    dn, dy, _ = out.stride()
+    rc = _native.lib().xrs_reproject_proj(
+        ptr(src), _native.DTYPE_CODES[_np_dtype(src)], n, plan.src_height, plan.src_width,
+        src_row0, h_band, sn, sy, ptr(out), _native.dtype_code(out_dtype), plan.dst_height,
+        plan.dst_width, r0, r1, dn, dy, plan.tile_height, plan.tile_width,
+        ptr(tabs["grid_x"]), ptr(tabs["grid_y"]), ctypes.cast(steps, ctypes.c_void_p), nsteps,
+        ptr(tabs["tile_x0"]), ptr(tabs["tile_y0"]), ptr(tabs["tile_win"]),
+        plan.win_height, plan.win_width, float(plan.x_res), float(plan.y_res), interp_code,
+        float(fill), flags.ptr, stream_handle(device, stream))
+    _native.check(rc, "xrs_reproject_proj")
     if own_flags and check:
         flags.raise_if_set("reproject")
     return out

@@ -69,11 +69,27 @@ class ReprojectPlan:
     grid_x: np.ndarray | None = None
     grid_y: np.ndarray | None = None
     transformer: Transformer | None = None
+    # 2-D plans: evaluate the transformation inside the gather
+    # (xrs_reproject_proj) instead of through coordinate tables; also chosen
+    # when the tables would exceed the ``reproject_table_max_bytes`` option
+    fuse_transform: bool = False
     _device_cache: dict = field(default_factory=dict, repr=False)
 
     @property
     def num_tiles(self) -> tuple[int, int]:
         return self.scr_ij_bboxes.shape[2], self.scr_ij_bboxes.shape[1]
+
+    def _tile_tables(self, device) -> dict:
+        key = ("tiles", str(device))
+        tabs = self._device_cache.get(key)
+        if tabs is None:
+            tabs = dict(
+                tile_x0=to_device(self.tile_x0.astype(np.float32), device),
+                tile_y0=to_device(self.tile_y0.astype(np.float32), device),
+                tile_win=to_device(np.ascontiguousarray(self.tile_win, np.int64), device),
+            )
+            self._device_cache[key] = tabs
+        return tabs
 
     def device_tables(self, device) -> dict:
         key = str(device)
@@ -86,13 +102,28 @@ class ReprojectPlan:
             else:
                 sx = to_device(np.ascontiguousarray(self.src_x, np.float64), device)
                 sy = to_device(np.ascontiguousarray(self.src_y, np.float64), device)
-            tabs = dict(
-                src_x=sx,
-                src_y=sy,
-                tile_x0=to_device(self.tile_x0.astype(np.float32), device),
-                tile_y0=to_device(self.tile_y0.astype(np.float32), device),
-                tile_win=to_device(np.ascontiguousarray(self.tile_win, np.int64), device),
-            )
+            tabs = dict(src_x=sx, src_y=sy, **self._tile_tables(device))
+            self._device_cache[key] = tabs
+        return tabs
+
+    def fused_transform(self, device) -> bool:
+        """True when the next K1 call evaluates the transformation per pixel:
+        a 2-D plan without coordinate tables on `device` whose tables would
+        exceed ``reproject_table_max_bytes`` (or ``fuse_transform`` set)."""
+        if self.coord_mode != 1 or self.src_x is not None or str(device) in self._device_cache:
+            return False
+        table_bytes = 16 * self.dst_width * self.dst_height
+        return self.fuse_transform or table_bytes > get_options()["reproject_table_max_bytes"]
+
+    def device_grid(self, device) -> dict:
+        """The target grid's pixel-centre axes + tile tables on `device`
+        (xrs_reproject_proj's inputs)."""
+        key = ("grid", str(device))
+        tabs = self._device_cache.get(key)
+        if tabs is None:
+            tabs = dict(grid_x=to_device(np.ascontiguousarray(self.grid_x, np.float64), device),
+                        grid_y=to_device(np.ascontiguousarray(self.grid_y, np.float64), device),
+                        **self._tile_tables(device))
             self._device_cache[key] = tabs
         return tabs
 
