@@ -89,3 +89,26 @@ def test_discovery_from_dataset():
     gm = xrs.GridMapping.from_dataset(dataset_5x5_regular_utm())
     assert gm.crs == xrs.CRS.from_epsg(32632)
     assert gm.xy_res == (100, 100) and gm.is_regular
+
+
+def test_webmerc_matches_published_epsg3857_constants():
+    """EPSG:3857 has no reference test (PROJ is absent and the reference's
+    tests never use it), so the spherical web Mercator restatement is checked
+    against constants published independently of this code: the EPSG
+    registry's projected bounds of EPSG:3857 (x = +-20037508.34 m at
+    lon = +-180, y = +-20048966.10 m at lat = +-85.06) and the square-world
+    latitude 85.0511287798066 deg, whose y equals pi * a = 20037508.342789244 m."""
+    from xcube_resampling_amd import crs
+
+    x, y = crs.webmerc_forward(np.array([180.0, -180.0, 0.0, 0.0, 0.0]),
+                               np.array([0.0, 0.0, 85.06, -85.06, 85.0511287798066]))
+    assert abs(x[0] - 20037508.34) < 0.005 and abs(x[1] + 20037508.34) < 0.005
+    assert abs(y[2] - 20048966.10) < 0.005 and abs(y[3] + 20048966.10) < 0.005
+    assert abs(y[4] - math.pi * 6378137.0) < 1e-6
+    assert x[2] == 0.0 and y[0] == 0.0
+    lon, lat = crs.webmerc_inverse(np.array([20037508.342789244]), np.array([20037508.342789244]))
+    assert abs(lon[0] - 180.0) < 1e-12 and abs(lat[0] - 85.0511287798066) < 1e-12
+    # the separable transformer of the bench pair (3857 -> 4326) uses these
+    tr = xrs.Transformer.from_crs("EPSG:3857", "EPSG:4326", always_xy=True)
+    assert tr.is_separable
+    np.testing.assert_array_equal(tr.transform_x(np.array([20037508.342789244])), [180.0])
