@@ -256,6 +256,22 @@ gather_separable_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t bands_
     for (int64_t sn = 0; sn < a.n; ++sn) {
       const T* __restrict__ src = static_cast<const T*>(a.src) + sn * a.src_sn;
       O* __restrict__ dst = static_cast<O*>(a.dst) + sn * a.dst_sn - g.row_begin * a.dst_sy + it.c0;
+      // stores are deferred by one batch: a store's data register stays
+      // busy until the store completes, so the previous batch's stores are
+      // issued after this batch's loads (they no longer hold the loads back)
+      O outv[kRows][kPx];
+      int64_t rprev = -1;
+      auto flush = [&](int64_t rp) {
+#pragma unroll
+        for (int q = 0; q < kRows; ++q) {
+          if (rp + q >= it.r1) break;
+#pragma unroll
+          for (int k = 0; k < kPx; ++k) {
+            const int lc = (int)threadIdx.x + k * kThreads;
+            if (lc < ncols) __builtin_nontemporal_store(outv[q][k], &dst[(rp + q) * a.dst_sy + lc]);
+          }
+        }
+      };
       for (int64_t r = it.r0; r < it.r1; r += kRows) {
         AxisEntry ye[kRows];
         T v[kRows][4][kPx];
@@ -278,28 +294,27 @@ gather_separable_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t bands_
             }
           }
         }
+        if (rprev >= 0) flush(rprev);
 #pragma unroll
         for (int q = 0; q < kRows; ++q) {
-          if (r + q >= it.r1) break;
           const bool okf = ye[q].f >= 0, okc = ye[q].c >= 0;
 #pragma unroll
           for (int k = 0; k < kPx; ++k) {
-            const int lc = (int)threadIdx.x + k * kThreads;
             const bool xf = cf[k] >= 0, xc = cc[k] >= 0;
             const T v00 = (okf && xf) ? v[q][0][k] : fill;
-            O out;
             if (INTERP == XRS_INTERP_NEAREST) {
-              out = (O)v00;
+              outv[q][k] = (O)v00;
             } else {
               const T v01 = (okf && xc) ? v[q][1][k] : fill;
               const T v10 = (okc && xf) ? v[q][2][k] : fill;
               const T v11 = (okc && xc) ? v[q][3][k] : fill;
-              out = Conv<O>::from_f64(interp4<T, INTERP>(v00, v01, v10, v11, dx[k], ye[q].d));
+              outv[q][k] = Conv<O>::from_f64(interp4<T, INTERP>(v00, v01, v10, v11, dx[k], ye[q].d));
             }
-            if (lc < ncols) __builtin_nontemporal_store(out, &dst[(r + q) * a.dst_sy + lc]);
           }
         }
+        rprev = r;
       }
+      if (rprev >= 0) flush(rprev);
     }
   }
 }
