@@ -104,3 +104,37 @@ def test_unknown_interp_method_raises():
     g = load_golden("reproject_f32.npz")
     with pytest.raises(NotImplementedError, match="interp_methods must be one of"):
         _oracle_run(g, "cubic")
+
+
+def test_non_separable_plan_fuses_only_above_table_budget():
+    """A 2-D (non-separable) plan keeps device coordinate tables unless they
+    would exceed the reproject_table_max_bytes option (or fuse_transform is
+    set); separable plans never fuse (host logic, no device needed)."""
+    import dataclasses
+
+    import xcube_resampling_amd as xrs
+
+    sgm = xrs.GridMapping.regular((300, 200), (400000.0, 5500000.0), 100.0, "EPSG:32632",
+                                  tile_size=128)
+    tgm = xrs.GridMapping.regular((250, 150), (4150000.0, 2950000.0), 100.0, "EPSG:3035",
+                                  tile_size=128)
+    plan = xrs.plan_reproject(sgm, tgm, xrs.Transformer.from_crs(tgm.crs, sgm.crs,
+                                                                 always_xy=True))
+    assert plan.coord_mode == 1 and plan.src_x is None
+    assert not plan.fused_transform("cuda:0")
+    with xrs.set_options(reproject_table_max_bytes=16 * 250 * 150 - 1):
+        assert plan.fused_transform("cuda:0")
+    with xrs.set_options(reproject_table_max_bytes=16 * 250 * 150):
+        assert not plan.fused_transform("cuda:0")
+    assert dataclasses.replace(plan, fuse_transform=True).fused_transform("cuda:0")
+    with pytest.raises(ValueError):
+        with xrs.set_options(reproject_table_max_bytes=-1):
+            pass
+    geo = xrs.GridMapping.regular((300, 200), (10.0, 50.0), 0.001, "EPSG:4326", tile_size=128)
+    merc = xrs.GridMapping.regular((250, 150), (1113195.0, 6446276.0), 100.0, "EPSG:3857",
+                                   tile_size=128)
+    sep = xrs.plan_reproject(geo, merc, xrs.Transformer.from_crs(merc.crs, geo.crs,
+                                                                 always_xy=True))
+    assert sep.coord_mode == 0
+    with xrs.set_options(reproject_table_max_bytes=0):
+        assert not sep.fused_transform("cuda:0")
