@@ -185,6 +185,25 @@ __device__ inline double interp4(T v00, T v01, T v10, T v11, double dx, double d
          (1.0 - dy) * Conv<T>::to_f64(Conv<T>::diff(v01, v11));
 }
 
+// A wave-uniform source row as a buffer resource (4 SGPRs): its taps are
+// buffer loads with a 32-bit lane byte offset — no 64-bit address per lane
+// (VALU and VGPRs the 16 tap rows of a batch no longer pay)
+__device__ inline __amdgpu_buffer_rsrc_t row_rsrc(const void* row, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(row), 0, (int)bytes, 0x00020000);
+}
+template <typename T>
+__device__ inline T row_at(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
+  if constexpr (sizeof(T) == 1) {
+    return __builtin_bit_cast(T, (uint8_t)__builtin_amdgcn_raw_buffer_load_b8(rs, off, 0, 0));
+  } else if constexpr (sizeof(T) == 2) {
+    return __builtin_bit_cast(T, (uint16_t)__builtin_amdgcn_raw_buffer_load_b16(rs, off, 0, 0));
+  } else if constexpr (sizeof(T) == 4) {
+    return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
+  } else {
+    return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 0));
+  }
+}
+
 struct GatherArgs {
   Geometry g;
   const void* src;
@@ -252,6 +271,14 @@ gather_separable_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t bands_
       cc[k] = e.c;
       dx[k] = e.d;
     }
+    const uint32_t row_bytes = (uint32_t)(g.src_w * (int64_t)sizeof(T));
+    // byte offsets of the tap columns in a row (< 2^31: checked at launch)
+    uint32_t fo[kPx], co[kPx];
+#pragma unroll
+    for (int k = 0; k < kPx; ++k) {
+      fo[k] = (uint32_t)max(cf[k], 0) * (uint32_t)sizeof(T);
+      co[k] = (uint32_t)max(cc[k], 0) * (uint32_t)sizeof(T);
+    }
     const AxisEntry* yt = a.ytab + it.t * g.tile_h - it.ty * g.tile_h;
     for (int64_t sn = 0; sn < a.n; ++sn) {
       const T* __restrict__ src = static_cast<const T*>(a.src) + sn * a.src_sn;
@@ -281,16 +308,17 @@ gather_separable_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t bands_
 #pragma unroll
         for (int q = 0; q < kRows; ++q) {
           ye[q] = (r + q < it.r1) ? yt[r + q] : AxisEntry{-1, -1, 0.0};
-          const T* rf = src + (int64_t)max(ye[q].f, 0) * a.src_sy;
-          const T* rc = src + (int64_t)max(ye[q].c, 0) * a.src_sy;
+          const __amdgpu_buffer_rsrc_t rf =
+              row_rsrc(src + (int64_t)max(ye[q].f, 0) * a.src_sy, row_bytes);
+          const __amdgpu_buffer_rsrc_t rc =
+              row_rsrc(src + (int64_t)max(ye[q].c, 0) * a.src_sy, row_bytes);
 #pragma unroll
           for (int k = 0; k < kPx; ++k) {
-            const int32_t f = max(cf[k], 0), c = max(cc[k], 0);
-            v[q][0][k] = rf[f];
+            v[q][0][k] = row_at<T>(rf, fo[k]);
             if (INTERP != XRS_INTERP_NEAREST) {
-              v[q][1][k] = rf[c];
-              v[q][2][k] = rc[f];
-              v[q][3][k] = rc[c];
+              v[q][1][k] = row_at<T>(rf, co[k]);
+              v[q][2][k] = row_at<T>(rc, fo[k]);
+              v[q][3][k] = row_at<T>(rc, co[k]);
             }
           }
         }
@@ -568,6 +596,12 @@ extern "C" int xrs_reproject(const void* src, int src_dtype, int64_t n, int64_t 
     return XRS_ERR_ARG;
   }
   if (row_begin == row_end) return XRS_OK;
+  // K1b addresses a source row through a buffer resource (byte extent < 2^31)
+  const int64_t esz = dispatch_dtype(src_dtype, [](auto tag) -> int { return (int)sizeof(tag); });
+  if (esz > 0 && src_w * esz > INT32_MAX) {
+    xrs_set_error("xrs_reproject: source rows above 2 GiB are not supported");
+    return XRS_ERR_ARG;
+  }
   if ((interp == XRS_INTERP_NEAREST || interp == XRS_INTERP_TRIANGULAR) && dst_dtype != src_dtype) {
     xrs_set_error("xrs_reproject: nearest/triangular output dtype must equal the source dtype");
     return XRS_ERR_ARG;
