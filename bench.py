@@ -197,7 +197,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    # untimed warm-up: the kernel trace of a fresh process shows the first
+    # ~15 launches 3-20 % slower than the steady state (profiles/r02_bench_kernel_trace.csv)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--size", type=int, default=40960)
     ap.add_argument("--tile", type=int, default=2048)
     ap.add_argument("--out-dtype", choices=["f32", "f64"], default="f32")
@@ -310,7 +312,7 @@ def main():
     if world == 1 and not args.no_f64 and out_np == np.float32:
         del out
         out64 = torch.empty((1, rows[1] - rows[0], args.size), device=device, dtype=torch.float64)
-        ms64, k64 = timed(make_step(out64, np.float64), max(5, args.steps // 2), 2)
+        ms64, k64 = timed(make_step(out64, np.float64), max(5, args.steps // 2), max(2, args.warmup // 2))
         flags.raise_if_set("bench reproject f64")
         b64 = 8 * (rows[1] - rows[0]) * args.size + 4 * s_read
         secondary = {"out_dtype": "f64 (the reference's bilinear dtype)",
