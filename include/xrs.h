@@ -110,6 +110,7 @@ int xrs_copy_async(void* dst, const void* src, int64_t bytes, void* stream);
  *      bilinear (the reference yields float64 there; float32 = declared dtype).
  * workspace: device scratch of xrs_reproject_workspace_size(...) bytes (the
  *      per-(tile, column) / (tile, row) index tables of coord_mode 0).
+ * A source row may span at most 2 GiB (src_w * element size), else XRS_ERR_ARG.
  * ------------------------------------------------------------------------- */
 int64_t xrs_reproject_workspace_size(int64_t dst_h, int64_t dst_w, int64_t tile_h,
                                      int64_t tile_w, int coord_mode);
