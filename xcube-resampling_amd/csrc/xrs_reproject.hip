@@ -51,6 +51,7 @@ constexpr int kPx = 2;                       // columns per thread
 constexpr int kSegW = kThreads * kPx;        // columns per work item
 constexpr int kBand = 32;                    // target rows per work item
 constexpr int kRows = 8;                     // target rows whose loads are in flight together
+constexpr int kRows2D = 2;                   // K1c: target rows per step (2-D tables; 4: slower)
 
 struct AxisEntry {   // one resolved column (or row) of one tile
   int32_t f;         // source index of floor(ix) (nearest: of rint(ix)); -1 = outside source
@@ -383,17 +384,73 @@ gather_2d_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t bands_per_til
     const int ncols = (int)(it.c1 - it.c0);
     const float x0 = g.tile_x0[it.t], y0 = g.tile_y0[it.t];
     const int64_t wi0 = g.tile_win[2 * it.t], wj0 = g.tile_win[2 * it.t + 1];
-    for (int64_t r = it.r0; r < it.r1; ++r) {
+    // kRows2D rows x kPx columns per step: their table entries, then every
+    // tap of a slice, are requested together (one dependent chain per step
+    // instead of per pixel)
+    for (int64_t r = it.r0; r < it.r1; r += kRows2D) {
+      bool ok[kRows2D][kPx];
+      double sx[kRows2D][kPx], sy[kRows2D][kPx];
 #pragma unroll
-      for (int k = 0; k < kPx; ++k) {
-        const int lc = (int)threadIdx.x + k * kThreads;
-        if (lc >= ncols) continue;
-        const int64_t p = r * g.dst_w + it.c0 + lc;
-        const AxisEntry ex = resolve_axis<INTERP>(g.src_x[p], x0, g.x_res, g.win_w, wi0, g.src_w,
-                                                  0, g.src_w, eflags);
-        const AxisEntry ey = resolve_axis<INTERP>(g.src_y[p], y0, g.neg_y_res, g.win_h, wj0,
-                                                  g.src_h, g.src_row0, g.src_rows, eflags);
-        gather_pixel<T, O, INTERP>(a, r, it.c0 + lc, ex, ey);
+      for (int q = 0; q < kRows2D; ++q)
+#pragma unroll
+        for (int k = 0; k < kPx; ++k) {
+          const int lc = (int)threadIdx.x + k * kThreads;
+          ok[q][k] = r + q < it.r1 && lc < ncols;
+          const int64_t p = ok[q][k] ? (r + q) * g.dst_w + it.c0 + lc : it.r0 * g.dst_w + it.c0;
+          sx[q][k] = g.src_x[p];
+          sy[q][k] = g.src_y[p];
+        }
+      AxisEntry ex[kRows2D][kPx], ey[kRows2D][kPx];
+#pragma unroll
+      for (int q = 0; q < kRows2D; ++q)
+#pragma unroll
+        for (int k = 0; k < kPx; ++k) {
+          ex[q][k] = ey[q][k] = AxisEntry{-1, -1, 0.0};
+          if (ok[q][k]) {
+            ex[q][k] = resolve_axis<INTERP>(sx[q][k], x0, g.x_res, g.win_w, wi0, g.src_w, 0,
+                                            g.src_w, eflags);
+            ey[q][k] = resolve_axis<INTERP>(sy[q][k], y0, g.neg_y_res, g.win_h, wj0, g.src_h,
+                                            g.src_row0, g.src_rows, eflags);
+          }
+        }
+      const T fill = Conv<T>::from_f64(a.fill);
+      for (int64_t sn = 0; sn < a.n; ++sn) {
+        const T* src = static_cast<const T*>(a.src) + sn * a.src_sn;
+        O* dst = static_cast<O*>(a.dst) + sn * a.dst_sn + (r - g.row_begin) * a.dst_sy + it.c0;
+        auto at = [&](int32_t row, int32_t c) -> T {
+          return src[(int64_t)max(row, 0) * a.src_sy + max(c, 0)];
+        };
+        T t[kRows2D][kPx][4];
+#pragma unroll
+        for (int q = 0; q < kRows2D; ++q)
+#pragma unroll
+          for (int k = 0; k < kPx; ++k) {
+            t[q][k][0] = at(ey[q][k].f, ex[q][k].f);
+            if (INTERP != XRS_INTERP_NEAREST) {
+              t[q][k][1] = at(ey[q][k].f, ex[q][k].c);
+              t[q][k][2] = at(ey[q][k].c, ex[q][k].f);
+              t[q][k][3] = at(ey[q][k].c, ex[q][k].c);
+            }
+          }
+#pragma unroll
+        for (int q = 0; q < kRows2D; ++q)
+#pragma unroll
+          for (int k = 0; k < kPx; ++k) {
+            if (!ok[q][k]) continue;
+            const AxisEntry& fx = ex[q][k];
+            const AxisEntry& fy = ey[q][k];
+            const T v00 = (fy.f >= 0 && fx.f >= 0) ? t[q][k][0] : fill;
+            O out;
+            if (INTERP == XRS_INTERP_NEAREST) {
+              out = (O)v00;
+            } else {
+              const T v01 = (fy.f >= 0 && fx.c >= 0) ? t[q][k][1] : fill;
+              const T v10 = (fy.c >= 0 && fx.f >= 0) ? t[q][k][2] : fill;
+              const T v11 = (fy.c >= 0 && fx.c >= 0) ? t[q][k][3] : fill;
+              out = Conv<O>::from_f64(interp4<T, INTERP>(v00, v01, v10, v11, fx.d, fy.d));
+            }
+            dst[q * a.dst_sy + (int)threadIdx.x + k * kThreads] = out;
+          }
       }
     }
   }
