@@ -66,3 +66,29 @@ def test_product_library_reads_no_environment():
                           capture_output=True, text=True, check=True).stdout
     assert "getenv" not in syms
     assert "secure_getenv" not in syms
+
+
+def test_argument_errors_are_reported_before_any_device_work():
+    """xrs_reproject / xrs_reproject_proj validate their arguments on the host
+    and return XRS_ERR_ARG with a message (no HIP call is made): a float64
+    source row above 2 GiB (K1 addresses rows as buffer resources) and an
+    unsupported projection pipeline."""
+    import ctypes
+
+    from xcube_resampling_amd import _native
+
+    lib = _native.load_library()
+    fake = ctypes.c_void_p(4096)   # never dereferenced: validation fails first
+    w = 300_000_000                # 2.4 GB per float64 row
+    rc = lib.xrs_reproject(fake, 11, 1, 4, w, 0, 4, 4 * w, w, fake, 11, 4, 4, 0, 4, 16, 4,
+                           4, 4, fake, fake, 0, fake, fake, fake, 4, 4, 1.0, 1.0, 0, 0.0,
+                           fake, 1 << 20, fake, None)
+    assert rc == _native.XRS_ERR_ARG
+    assert b"2 GiB" in lib.xrs_last_error()
+    steps = (_native.ProjStep * 2)()
+    steps[0].kind, steps[1].kind = 1, 3   # forward then forward: not a pipeline
+    rc = lib.xrs_reproject_proj(fake, 10, 1, 4, 4, 0, 4, 16, 4, fake, 10, 4, 4, 0, 4, 16, 4,
+                                4, 4, fake, fake, ctypes.cast(steps, ctypes.c_void_p), 2,
+                                fake, fake, fake, 4, 4, 1.0, 1.0, 0, 0.0, fake, None)
+    assert rc == _native.XRS_ERR_ARG
+    assert b"pipeline" in lib.xrs_last_error()
