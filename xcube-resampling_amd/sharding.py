@@ -61,8 +61,11 @@ class BandShard:
 
 # K1 time per band on MI355X ~ rows + COST_SRC_ROW_WEIGHT x source rows read
 # (least-squares fit over the per-rank kernel times of the one-GPU rehearsal
-# of 1/2/4/8-way splits of config 5: profiles/r02_band_rehearsal.jsonl)
-COST_SRC_ROW_WEIGHT = 0.147
+# of 2/4/8-way splits of config 5 with the round-2 kernel — buffer-resource
+# taps, deferred stores: 4.57e-5 ms per target row + 1.75e-5 ms per source
+# row + 0.02 ms per launch, profiles/r02_band_rehearsal.jsonl; 0.147 fitted
+# the round-1 kernel)
+COST_SRC_ROW_WEIGHT = 0.37
 
 
 def band_splits(plan, world: int, balance: str = "rows", out_itemsize: int = 4) -> list[int]:
