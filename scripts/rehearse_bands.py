@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--worlds", type=int, nargs="+", default=[1, 2, 4, 8])
     ap.add_argument("--balance", nargs="+", default=["rows", "cost"])
     ap.add_argument("--reps", type=int, default=15)
+    ap.add_argument("--warm", type=int, default=20)
     a = ap.parse_args()
 
     import torch
@@ -53,7 +54,8 @@ def main():
                 run = lambda: kernels.reproject(src, plan, "bilinear", np.nan,  # noqa: E731
                                                 out_dtype=np.float32, out=out, rows=sh.rows,
                                                 src_row0=j0, flags=flags, check=False)
-                run()
+                for _ in range(a.warm):   # steady state before timing (the first
+                    run()                   # launches on a fresh band run slower)
                 torch.cuda.synchronize()
                 # back-to-back launches between two events (the host's launch
                 # latency is hidden, as in the bench's graph replay); median of 5
