@@ -105,15 +105,19 @@ def test_config5_band_balance(world):
 
     _, _, plan, _, _ = bench.workload(40960, 2048)
     cols = plan.source_cols_read()
-    from xcube_resampling_amd.sharding import COST_SRC_ROW_WEIGHT
+    from xcube_resampling_amd.sharding import COST_DUP_ROW_WEIGHT, COST_SRC_ROW_WEIGHT
 
+    lo, hi = plan.row_source_extent()
+    valid = hi >= lo
+    dup = np.zeros(len(lo), bool)
+    dup[1:] = (lo[1:] == lo[:-1]) & valid[1:] & valid[:-1]
     for balance in ("rows", "bytes", "cost"):
         shards = [band_shard(plan, world, r, balance) for r in range(world)]
         nrows = np.array([s.row1 - s.row0 for s in shards], float)
         alg = np.array([4 * 40960 * (s.row1 - s.row0) + 4 * cols * (s.src_row1 - s.src_row0)
                         for s in shards], float)
         cost = np.array([(s.row1 - s.row0) + COST_SRC_ROW_WEIGHT * (s.src_row1 - s.src_row0)
-                         for s in shards])
+                         + COST_DUP_ROW_WEIGHT * dup[s.row0:s.row1].sum() for s in shards])
         if balance == "rows":
             assert nrows.max() / nrows.mean() <= 1.0 + 1e-9
         elif balance == "bytes":

@@ -60,12 +60,15 @@ class BandShard:
 
 
 # K1 time per band on MI355X ~ rows + COST_SRC_ROW_WEIGHT x source rows read
-# (least-squares fit over the per-rank kernel times of the one-GPU rehearsal
-# of 2/4/8-way splits of config 5 with the round-2 kernel — buffer-resource
-# taps, deferred stores: 4.57e-5 ms per target row + 1.75e-5 ms per source
-# row + 0.02 ms per launch, profiles/r02_band_rehearsal.jsonl; 0.147 fitted
-# the round-1 kernel)
-COST_SRC_ROW_WEIGHT = 0.37
+# + COST_DUP_ROW_WEIGHT x target rows whose floor source row repeats the
+# previous row's (their requests duplicate lines still in flight: the bands
+# near 70 N, where a source row serves ~1.6 target rows, ran 3-5 % above the
+# two-term model).  Least-squares fit over the per-rank kernel times of the
+# one-GPU rehearsals of 2/4/8-way splits with the round-2 kernel
+# (3.45e-5 ms per target row, 2.56e-5 per source row, 1.55e-5 per repeated
+# row, 0.023 ms per launch; profiles/r02_band_rehearsal*.jsonl).
+COST_SRC_ROW_WEIGHT = 0.74
+COST_DUP_ROW_WEIGHT = 0.45
 
 
 def band_splits(plan, world: int, balance: str = "rows", out_itemsize: int = 4) -> list[int]:
@@ -79,8 +82,10 @@ def band_splits(plan, world: int, balance: str = "rows", out_itemsize: int = 4) 
                      source rows it reads: at config 5 a target row near 30 N
                      reads 2.6x the source rows of one near 70 N);
     balance="cost":  equal measured K1 time: rows + COST_SRC_ROW_WEIGHT x
-                     source rows (the gather is bound by target pixels more
-                     than by source bytes: equal bytes over-corrects)."""
+                     source rows + COST_DUP_ROW_WEIGHT x rows repeating the
+                     previous row's floor source row (the gather is bound by
+                     target pixels more than by source bytes: equal bytes
+                     over-corrects)."""
     h = plan.dst_height
     if world < 1:
         raise ValueError(f"invalid world size {world}")
@@ -101,6 +106,10 @@ def band_splits(plan, world: int, balance: str = "rows", out_itemsize: int = 4) 
     run_hi = np.maximum.accumulate(np.where(valid, hi, first - 1))
     src_rows = np.concatenate([[0], np.maximum(run_hi - first + 1, 0)])
     f = row_w * np.arange(h + 1) + src_w * src_rows
+    if balance == "cost":   # + repeated floor rows (see COST_DUP_ROW_WEIGHT)
+        dup = np.zeros(h, bool)
+        dup[1:] = (lo[1:] == lo[:-1]) & valid[1:] & valid[:-1]
+        f = f + COST_DUP_ROW_WEIGHT * np.concatenate([[0], np.cumsum(dup)])
     targets = f[-1] * np.arange(1, world) / world
     cuts = np.searchsorted(f, targets, side="left")
     return [0] + [int(c) for c in cuts] + [h]
