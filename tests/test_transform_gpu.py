@@ -172,6 +172,54 @@ def test_fused_projection_gather_equals_tables_path(src_crs, dst_crs, dtype, int
     assert str(src.device) not in fused._device_cache   # no coordinate tables were made
 
 
+def test_streamed_host_source_fuses_when_tables_exceed_budget():
+    """A host-resident source (band pipeline of streaming.reproject_host) on a
+    non-separable pair with the table budget at 0: the projection runs inside
+    the gather — no 2-D coordinate tables are uploaded — and the result equals
+    the table path bit for bit (the pre-upload ignored the
+    budget)."""
+    import torch
+
+    import xcube_resampling_amd as xrs
+    from xcube_resampling_amd import kernels
+
+    n = 600
+    tgm = xrs.GridMapping.regular((500, 400), (4150000.0, 2950000.0), 100.0, "EPSG:3035",
+                                  tile_size=128)
+    a = np.random.default_rng(6).random((2, n, n)).astype(np.float32)
+    x = 400000.0 + (np.arange(n) + 0.5) * 100.0
+    y = 5500000.0 + (np.arange(n)[::-1] + 0.5) * 100.0
+    sgm = xrs.GridMapping.from_coords(xrs.DataArray(x, "x", name="x"),
+                                      xrs.DataArray(y, "y", name="y"), "EPSG:32632")
+
+    def run():
+        ds = xrs.Dataset(data_vars={"v": (("t", "y", "x"), a)},
+                         coords={"x": ("x", x), "y": ("y", y)})
+        with xrs.set_options(host_streaming_min_bytes=0):
+            return xrs.reproject_dataset(ds, tgm, source_gm=sgm, interp_methods="bilinear")["v"]
+
+    calls = []
+    orig = kernels._reproject_proj
+
+    def spy(*args, **kw):
+        calls.append(1)
+        return orig(*args, **kw)
+
+    kernels._reproject_proj = spy
+    try:
+        ref = run().values
+        assert not calls
+        with xrs.set_options(reproject_table_max_bytes=0):
+            got = run().values
+        assert calls   # every band through xrs_reproject_proj
+    finally:
+        kernels._reproject_proj = orig
+    assert isinstance(ref, np.ndarray) and isinstance(got, np.ndarray)   # host in, host out
+    assert np.isfinite(ref).mean() > 0.5
+    assert np.array_equal(ref, got, equal_nan=True)
+    torch.cuda.synchronize()
+
+
 def test_reproject_dataset_fuses_when_tables_exceed_budget():
     """reproject_dataset on a non-separable pair: with the table budget at 0
     the projection runs inside the gather (no coordinate tables are made),

@@ -159,7 +159,14 @@ def reproject_host(src: np.ndarray, plan, interp: str, fill: float, out_dtype=No
     cur = t.cuda.current_stream(device)
     s_in, s_k, s_out = (t.cuda.Stream(device) for _ in range(3))
     flags = kernels.ErrorFlags(device)
-    plan.device_tables(device)   # uploaded on the current stream, before the others start
+    # the plan's device inputs are uploaded on the current stream, before the
+    # others start: the grid axes when the transformation is fused into the
+    # gather (no 2-D coordinate tables: reproject_table_max_bytes holds here
+    # too), else the coordinate tables
+    if plan.fused_transform(device):
+        plan.device_grid(device)
+    else:
+        plan.device_tables(device)
     for s in (s_in, s_k, s_out):
         s.wait_stream(cur)
     row_src, row_dst = w * src.itemsize, wd * out_dtype.itemsize
