@@ -13,6 +13,14 @@ rows — independent partitions, no data-path collective, "scaling": "strong".
 ``--shard slices`` instead gives rank r its own whole raster (weak scaling).
 
 `value` = target pixels of the whole job / max-over-ranks wall time.
+Before the warm-up steps each rank measures the device-copy rate of its
+source band (benchlib: a streaming float4 copy, the fastest shape measured on
+MI355X, profiles/r03_region_copy.jsonl): `roofline.copy_GBs` /
+`frac_of_copy`.  Those ~0.1 s of copies also bring the shader
+clock from its idle level to the loaded one: the chip's DVFS needs ~30 ms of
+load to ramp from ~1.6 to ~2.38 GHz and K1 follows the clock
+(profiles/r03_ramp_probe.jsonl, r03_ramp_pmc_clock.csv); `clock_GHz` gives
+the clock measured just before and just after the timed steps.
 `roofline.achieved` = algorithmic bytes of all ranks (output + distinct
 source pixels read, x4 B) / max-over-ranks kernel time (HIP events on the
 launch stream); `peak` = N x 8 TB/s.  `traffic` = FETCH_SIZE + WRITE_SIZE per
@@ -107,11 +115,15 @@ def synthetic_rows(j0: int, j1: int, width: int, device, seed: int = 20250905):
     return out
 
 
-def cpu_baseline(plan, tgm, seconds: float = 12.0):
+def cpu_baseline(plan, tgm, seconds: float = 12.0, sweep=(1, 32, 128), sweep_seconds=3.0):
     """Oracle (numpy restatement of reproject.py:268-335 + the per-tile window
-    copy of 499-530 + the per-pixel transform of 472-496) on ALL host cores:
+    copy of 499-530 + the per-pixel transform of 472-496) on host threads:
     one task per 2048^2 target tile on a thread pool (the dask threaded
-    scheduler's shape), tiles taken from every tile row, for `seconds`."""
+    scheduler's shape), tiles taken from every tile row.  All cores of the
+    affinity mask for `seconds`, plus a thread-count sweep (`sweep_seconds`
+    each): numpy releases the GIL only inside its inner loops, so like
+    dask's threaded scheduler the port scales far below linearly; `value` is
+    the best rate of the sweep."""
     from concurrent.futures import ThreadPoolExecutor
 
     from oracle import gridmapping_ref as gref
@@ -141,21 +153,36 @@ def cpu_baseline(plan, tgm, seconds: float = 12.0):
                                           plan.y_res, "bilinear")
         return (r1 - r0) * (c1 - c0)
 
-    px = 0
-    t0 = time.perf_counter()
-    with ThreadPoolExecutor(max_workers=cores) as ex:
-        k = 0
-        while time.perf_counter() - t0 < seconds:
-            batch = [tiles[(k + q) % len(tiles)] for q in range(cores)]
-            k += cores
-            px += sum(ex.map(run_tile, batch))
-    dt = time.perf_counter() - t0
-    return dict(value=round(px / dt / 1e6, 2), unit="Mpixels/s", cores=cores, kind="port",
-                sample=f"{px // (plan.tile_width * plan.tile_height)} target tiles of "
-                       f"{plan.tile_width}x{plan.tile_height} taken across all tile rows "
-                       f"(bilinear, f32 in, f64 out as the reference) in {dt:.1f} s, incl. "
-                       f"per-pixel coordinate transform and window copy; numpy oracle, one "
-                       f"task per tile on a {cores}-thread pool (all cores of the affinity mask)")
+    def rate(threads, secs):
+        px, k = 0, 0
+        t0 = time.perf_counter()
+        with ThreadPoolExecutor(max_workers=threads) as ex:
+            while time.perf_counter() - t0 < secs:
+                batch = [tiles[(k + q) % len(tiles)] for q in range(threads)]
+                k += threads
+                px += sum(ex.map(run_tile, batch))
+        dt = time.perf_counter() - t0
+        return px / dt / 1e6, px, dt
+
+    rates = {}
+    for n in sweep:
+        if n < cores:
+            rates[n] = round(rate(n, sweep_seconds)[0], 2)
+    all_rate, px, dt = rate(cores, seconds)
+    rates[cores] = round(all_rate, 2)
+    best = max(rates, key=rates.get)
+    return dict(value=rates[best], unit="Mpixels/s", cores=best, kind="port",
+                threads_sweep={str(k): v for k, v in sorted(rates.items())},
+                per_thread_Mpx_s=round(rates[best] / best, 3),
+                sample=f"numpy oracle of the reference's per-tile path (bilinear, f32 in, f64 out "
+                       f"as the reference, incl. per-pixel coordinate transform and window copy), "
+                       f"one task per {plan.tile_width}x{plan.tile_height} target tile on a "
+                       f"thread pool, tiles taken across all tile rows; {cores} threads "
+                       f"(all cores of the affinity mask) for {dt:.1f} s "
+                       f"({px // (plan.tile_width * plan.tile_height)} tiles) plus "
+                       f"{sweep_seconds:.0f} s per point of the thread sweep; value = the best "
+                       f"point ({best} threads): GIL-bound like dask's threaded scheduler "
+                       f"(numpy releases the GIL only inside its inner loops)")
 
 
 def measure_traffic(size: int, tile: int, out_dtype: str, timeout: int = 170):
@@ -193,6 +220,61 @@ def measure_traffic(size: int, tile: int, out_dtype: str, timeout: int = 170):
         shutil.rmtree(d, ignore_errors=True)
 
 
+def load_benchlib():
+    """benchlib/libxrs_bench.so (measurement support; built by build())."""
+    import ctypes
+
+    lib = ctypes.CDLL(os.path.join(ROOT, "benchlib", "libxrs_bench.so"))
+    lib.xrs_bench_copy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                   ctypes.c_int, ctypes.c_void_p]
+    lib.xrs_bench_clock_probe.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                          ctypes.c_void_p]
+    return lib
+
+
+COPY_VARIANT = 2   # one float4 per thread, one 4 KiB block per 256 threads: 6.2 TB/s
+
+
+def device_copy_rate(lib, src, stream, warm: int = 40, timed: int = 20) -> float:
+    """GB/s (read + write) of a streaming copy of `src` into a scratch buffer of
+    the same size, on `stream`; the first `warm` copies are untimed."""
+    import torch
+
+    nbytes = src.numel() * src.element_size()
+    if nbytes == 0:
+        return 0.0
+    scratch = torch.empty_like(src)
+    sh = int(stream.cuda_stream)
+
+    def copy():
+        if lib.xrs_bench_copy(src.data_ptr(), scratch.data_ptr(), nbytes, COPY_VARIANT, sh) != 0:
+            raise RuntimeError("benchlib copy failed")
+
+    for _ in range(warm):
+        copy()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(timed):
+        copy()
+    e1.record(stream)
+    e1.synchronize()
+    ms = e0.elapsed_time(e1) / timed
+    del scratch
+    return 2 * nbytes / (ms / 1e3) / 1e9
+
+
+def shader_clock_ghz(lib, stream, blocks: int = 1024, spin: int = 3000) -> float:
+    """Median over blocks of d(s_memtime) / d(s_memrealtime) x 100 MHz."""
+    import torch
+
+    buf = torch.zeros((blocks, 2), dtype=torch.int64, device=stream.device)
+    if lib.xrs_bench_clock_probe(buf.data_ptr(), blocks, spin, int(stream.cuda_stream)) != 0:
+        raise RuntimeError("benchlib clock probe failed")
+    stream.synchronize()
+    d = buf.cpu().numpy()
+    return round(float(np.median(d[:, 0] / np.maximum(d[:, 1], 1))) * 0.1, 3)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -217,8 +299,10 @@ def main():
                          "slices: rank r reprojects its own raster (weak)")
     ap.add_argument("--balance", choices=["rows", "bytes", "cost"], default="cost",
                     help="row-band split: equal target rows, equal algorithmic bytes, or "
-                         "equal measured K1 cost (sharding.band_splits; the default: "
-                         "max/mean 1.008 at 8 ranks in profiles/r02_band_rehearsal.jsonl)")
+                         "equal predicted K1 cost (sharding.band_splits; the default, weights "
+                         "fitted in-sample to one-GPU rehearsals: max/mean 1.015 at 8 ranks in "
+                         "profiles/r02_band_rehearsal.jsonl; N > 1 lines report every model's "
+                         "prediction next to the measured per-rank times)")
     args = ap.parse_args()
 
     from xcube_resampling_amd.sharding import band_shard, env_rank, max_over_ranks
@@ -228,6 +312,11 @@ def main():
     traffic = None
     if world == 1 and not args.no_traffic:
         traffic = measure_traffic(args.size, args.tile, args.out_dtype)
+    src_gm, tgm, plan, lon, lat = workload(args.size, args.tile)   # host only
+    # the CPU baseline runs before HIP is initialised (host threads only)
+    cpu = None
+    if world == 1 and rank == 0 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(plan, tgm, args.cpu_seconds)
 
     import torch
     import torch.distributed as dist
@@ -247,7 +336,6 @@ def main():
         else:
             dist.init_process_group(backend)
 
-    src_gm, tgm, plan, lon, lat = workload(args.size, args.tile)
     out_np = np.float32 if args.out_dtype == "f32" else np.float64
     if args.shard == "bands":
         shard = band_shard(plan, world, rank, args.balance, np.dtype(out_np).itemsize)
@@ -257,6 +345,9 @@ def main():
         rows, (j0, j1) = (0, plan.dst_height), (0, plan.src_height)
         src = synthetic_rows(0, plan.src_height, args.size, device, seed=20250905 + 1000 * rank)
     flags = kernels.ErrorFlags(device)
+    benchlib = load_benchlib()
+    stream = torch.cuda.current_stream(device)   # the stream the kernels run on
+    copy_gbs = device_copy_rate(benchlib, src, stream)
 
     def make_step(out, dtype):
         def step():
@@ -285,9 +376,9 @@ def main():
         for _ in range(warmup):
             run()
         torch.cuda.synchronize()
+        clk0 = shader_clock_ghz(benchlib, stream)   # outside the timed region
         barrier()
         torch.cuda.synchronize()
-        stream = torch.cuda.current_stream(device)   # the stream the kernels run on
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
         ev0.record(stream)
@@ -297,12 +388,13 @@ def main():
         torch.cuda.synchronize()
         barrier()
         t1 = time.perf_counter()
+        clk1 = shader_clock_ghz(benchlib, stream)
         wall = max_over_ranks(t1 - t0, device) / steps * 1e3
-        return wall, ev0.elapsed_time(ev1) / steps
+        return wall, ev0.elapsed_time(ev1) / steps, (clk0, clk1)
 
     out = torch.empty((1, rows[1] - rows[0], args.size), device=device,
                       dtype=torch.float32 if out_np == np.float32 else torch.float64)
-    ms_per_step, kernel_ms = timed(make_step(out, out_np), args.steps, args.warmup)
+    ms_per_step, kernel_ms, clocks = timed(make_step(out, out_np), args.steps, args.warmup)
     flags.raise_if_set("bench reproject")
 
     s_read = source_pixels_read(plan, rows) if rows[1] > rows[0] else 0
@@ -312,7 +404,8 @@ def main():
     if world == 1 and not args.no_f64 and out_np == np.float32:
         del out
         out64 = torch.empty((1, rows[1] - rows[0], args.size), device=device, dtype=torch.float64)
-        ms64, k64 = timed(make_step(out64, np.float64), max(5, args.steps // 2), max(2, args.warmup // 2))
+        ms64, k64, _ = timed(make_step(out64, np.float64), max(5, args.steps // 2),
+                             max(2, args.warmup // 2))
         flags.raise_if_set("bench reproject f64")
         b64 = 8 * (rows[1] - rows[0]) * args.size + 4 * s_read
         secondary = {"out_dtype": "f64 (the reference's bilinear dtype)",
@@ -323,14 +416,22 @@ def main():
                      "frac": round(b64 / (k64 / 1e3) / 1e9 / HBM_PEAK_GBS, 4)}
         del out64
 
-    if world > 1:   # whole-job bytes, slowest rank's kernel time
+    rank_ms = None
+    if world > 1:   # whole-job bytes, slowest rank's kernel time, every rank's time
         t = torch.tensor([float(my_bytes)], dtype=torch.float64,
                          device=device if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         alg_bytes = float(t.item())
         max_kernel_ms = max_over_ranks(kernel_ms, device)
+        cdev = device if backend == "nccl" else "cpu"
+        parts = [torch.zeros(2, dtype=torch.float64, device=cdev) for _ in range(world)]
+        dist.all_gather(parts, torch.tensor([kernel_ms, copy_gbs], dtype=torch.float64,
+                                            device=cdev))
+        rank_ms = [round(float(p[0]), 4) for p in parts]
+        copy_all = float(sum(float(p[1]) for p in parts))
     else:
         alg_bytes, max_kernel_ms = float(my_bytes), kernel_ms
+        copy_all = copy_gbs
     n_rasters = world if args.shard == "slices" else 1
     value = n_rasters * args.size * args.size / (ms_per_step / 1e3) / 1e6
     peak = HBM_PEAK_GBS * world
@@ -377,17 +478,33 @@ def main():
                 "kernel": "gather_separable_kernel<float,float,1> (+ axis_tables_kernel<1>, <1%)",
                 "kernel_ms": round(max_kernel_ms, 4),
                 "algorithmic_bytes": int(alg_bytes),
+                "copy_GBs": round(copy_all, 1),
+                "frac_of_copy": round(achieved / copy_all, 4),
+                "copy": "same-run streaming float4 copy of each rank's source band (read + "
+                        "write bytes / time; benchlib xrs_bench_copy), summed over ranks",
                 "scope": "whole job: bytes of all ranks / slowest rank's kernel time; "
                          "peak = n_gpus x 8 TB/s",
             },
         }
+        res["clock_GHz"] = {"before_timed": clocks[0], "after_timed": clocks[1],
+                            "note": "rank 0 shader clock (s_memtime / s_memrealtime probe) "
+                                    "right outside the timed region"}
+        if rank_ms is not None:
+            from xcube_resampling_amd.sharding import band_splits, split_predictions
+            res["ranks"] = {"kernel_ms": rank_ms,
+                            "max_over_mean": round(max(rank_ms) / (sum(rank_ms) / world), 4)}
+            if args.shard == "bands":
+                cuts = band_splits(plan, world, args.balance, np.dtype(out_np).itemsize)
+                res["ranks"]["cuts"] = cuts
+                res["ranks"]["predicted"] = split_predictions(plan, cuts,
+                                                              np.dtype(out_np).itemsize)
         if traffic:
             res["roofline"]["traffic_detail"] = {
                 k: traffic[k] for k in ("read_bytes", "write_bytes", "calibration")}
         if secondary:
             res["f64_out"] = secondary
-        if world == 1 and not args.no_cpu_baseline:
-            res["cpu_baseline"] = cpu_baseline(plan, tgm, args.cpu_seconds)
+        if cpu is not None:
+            res["cpu_baseline"] = cpu
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -59,6 +59,8 @@ extern "C" {
 #define XRS_EFLAG_BAND 2      /* read outside the source band held on device  */
 #define XRS_EFLAG_NAN_TO_INT 4  /* int(nan): coarsen mode on a float chunk with NaN (ValueError) */
 #define XRS_EFLAG_INF_TO_INT 8  /* int(+-inf): coarsen mode, infinite values (OverflowError)   */
+#define XRS_EFLAG_STATE 16    /* rectify: a tile record, claim key or source position outside
+                                 its raster (inconsistent inputs); the access was skipped  */
 
 /* library identification */
 const char* xrs_version(void);
@@ -257,7 +259,8 @@ int xrs_rectify_ij(const double* x, const double* y, int64_t h, int64_t w, int64
                    const void* tiles, int64_t ntiles, int64_t ntiles_x,
                    const int64_t* chunk_offsets, int64_t max_chunks,
                    int64_t dst_h, int64_t dst_w, double x_scale, double y_scale,
-                   double uv_delta, uint32_t* keys, double* ij, void* stream);
+                   double uv_delta, uint32_t* keys, double* ij, int32_t* err_flags,
+                   void* stream);
 
 /* -------------------------------------------------------------------------
  * xrs_rectify_tiles — the host-side tiling of _compute_target_source_ij
@@ -288,7 +291,7 @@ int xrs_rectify_tiles(const int32_t* acc, int64_t ntiles_x, int64_t ntiles_y, in
 int xrs_rectify_var(const double* ij, int64_t ij_sn, int64_t dst_h, int64_t dst_w, const void* src,
                     int src_dtype, int64_t n, int64_t src_h, int64_t src_w, int64_t src_sn,
                     int64_t src_sy, void* dst, int64_t dst_sn, int interp, double fill,
-                    void* stream);
+                    int32_t* err_flags, void* stream);
 
 /* -------------------------------------------------------------------------
  * Test-only path selection.  Every kernel has ONE schedule per case; these

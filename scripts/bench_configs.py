@@ -319,25 +319,27 @@ def config4(args):
 
     tiles, ntx, bb, _ = R.rectify_tiles(sgm, tgm, xy=xy)
     dst_y_scale = -tgm.y_res
+    flags = kernels.ErrorFlags(src.device)   # checked once at the end (no sync per call)
 
     def k5():
         return kernels.rectify_ij(xy[0], xy[1], tiles, ntx, tgm.height, tgm.width, tgm.x_res,
-                                  dst_y_scale, 1e-3)
+                                  dst_y_scale, 1e-3, flags=flags)
 
     ij = k5()
     covered = int(torch.sum(~torch.isnan(ij[0])).item())
     k5_ms, _ = _timed(k5, args.steps, args.warmup)
     lines = {}
     for interp in ("nearest", "bilinear"):
-        k6_ms, _ = _timed(lambda: kernels.rectify_var(ij, src, interp, float("nan")),
+        k6_ms, _ = _timed(lambda: kernels.rectify_var(ij, src, interp, float("nan"),
+                                                      flags=flags),
                           args.steps, args.warmup)
         lines[interp] = k6_ms
 
     def pipeline(interp):   # K4 -> device tiling -> K5 -> K6, no host round trip
         t = R._device_tiles(sgm, tgm, xy)
         ij_ = kernels.rectify_ij(xy[0], xy[1], t, ntx, tgm.height, tgm.width, tgm.x_res,
-                                 dst_y_scale, 1e-3)
-        return kernels.rectify_var(ij_, src, interp, float("nan"))
+                                 dst_y_scale, 1e-3, flags=flags)
+        return kernels.rectify_var(ij_, src, interp, float("nan"), flags=flags)
 
     # the device tiling reproduces the host tiling byte for byte
     t_dev, offs = R._device_tiles(sgm, tgm, xy)
@@ -379,6 +381,7 @@ def config4(args):
                           "kernels, tiles on a thread pool)"),
               {"covered_px": covered, "k5_ms": round(k5_ms, 4),
                "k6_ms": round(lines[interp], 4)})
+    flags.raise_if_set("config 4")
 
 
 def main():

@@ -262,11 +262,15 @@ def test_integral_coarsen_slow_list(nan_frac, order):
 
 def test_config3_full_size_sampled_blocks():
     """BASELINE config 3 at full size — coarsen mean 4x4 of a 16384^2 float32
-    raster (K3i, one launch): 1024^2-source blocks at the corners and the centre
-    == the oracle (dask-image chunk footprint + scipy order 1 + numpy nanmean
-    in dask chunk.coarsen order) on the same block, bit for bit (the block's
-    own last output row/column excluded: there the standalone block mirrors its
-    edge, the full raster does not)."""
+    raster with 0.1 % NaN (K3i, one launch): 1024^2-source blocks at the
+    corners, the centre and across an output-chunk seam == the oracle
+    (dask-image chunk footprint + scipy order 1 + numpy nanmean in dask
+    chunk.coarsen order), bit for bit, EVERY output row and column of the block
+    included: the oracle runs on the block plus a one-output-pixel source halo
+    (4 rows / columns) where the raster continues, so the block's last
+    row/column (an interior seam of the full raster) sees the same
+    neighbours — including the zero-weight NaN taps of the next block — as the
+    one-launch result does."""
     import torch
 
     import xcube_resampling_amd.affine as A
@@ -278,16 +282,18 @@ def test_config3_full_size_sampled_blocks():
     gen = torch.Generator(device="cuda")
     gen.manual_seed(9)
     src = torch.rand((1, n, n), generator=gen, device="cuda", dtype=torch.float32)
+    src[torch.rand((1, n, n), generator=gen, device="cuda") < 0.001] = float("nan")
     plan = A.plan_affine(tuple(src.shape), np.dtype(np.float32), m, (1, n // k, n // k),
                          (1, 512, 512), 1, "mean", False, np.nan)
     out = kernels.affine(src, plan)
     c = 1024
-    for r0, c0 in [(0, 0), (0, n - c), (n // 2, n // 2), (n - c, 0), (n - c, n - c)]:
-        a = src[:, r0:r0 + c, c0:c0 + c].cpu().numpy()
-        ref = affine_ref.resample_array(a, m, (1, c // k, c // k), (1, c // k, c // k), 1,
-                                        "mean", False, np.nan)
+    # (1536, 3584): output rows 384-639 straddle the 512-row output chunk seam
+    for r0, c0 in [(0, 0), (0, n - c), (n // 2 - c // 2, n // 2 - c // 2), (1536, 3584),
+                   (n - c, 0), (n - c, n - c)]:
+        r1, c1 = min(n, r0 + c + k), min(n, c0 + c + k)
+        a = src[:, r0:r1, c0:c1].cpu().numpy()
+        oh, ow = (r1 - r0) // k, (c1 - c0) // k
+        ref = affine_ref.resample_array(a, m, (1, oh, ow), (1, oh, ow), 1, "mean", False, np.nan)
         got = out[:, r0 // k:(r0 + c) // k, c0 // k:(c0 + c) // k].cpu().numpy()
-        last = r0 + c == n, c0 + c == n   # the raster's own edge: mirrored in both
-        assert_bitwise_equal(got[:, :None if last[0] else -1, :None if last[1] else -1],
-                             ref[:, :None if last[0] else -1, :None if last[1] else -1],
-                             f"block at ({r0}, {c0})")
+        assert np.isnan(a).any(), "the sample must exercise the NaN path"
+        assert_bitwise_equal(got, np.asarray(ref)[:, :c // k, :c // k], f"block at ({r0}, {c0})")

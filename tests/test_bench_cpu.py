@@ -24,13 +24,34 @@ def test_source_pixels_read_matches_band_sum():
     assert total <= sum(parts) <= total + 4 * 2 * plan.source_cols_read()
 
 
-def test_cpu_baseline_runs_on_all_cores():
+def test_cpu_baseline_thread_sweep():
+    """The CPU baseline runs all cores plus a thread sweep; `value` is the best
+    point and `cores` the thread count it used."""
     import bench
 
     _, tgm, plan, _, _ = bench.workload(2048, 512)
-    cpu = bench.cpu_baseline(plan, tgm, seconds=0.5)
-    assert cpu["cores"] == len(os.sched_getaffinity(0))
-    assert cpu["value"] > 0 and cpu["kind"] == "port"
+    cpu = bench.cpu_baseline(plan, tgm, seconds=0.5, sweep=(1, 2), sweep_seconds=0.3)
+    allc = len(os.sched_getaffinity(0))
+    sweep = {int(k): v for k, v in cpu["threads_sweep"].items()}
+    assert allc in sweep and all(v > 0 for v in sweep.values())
+    assert cpu["value"] == max(sweep.values()) and sweep[cpu["cores"]] == cpu["value"]
+    assert cpu["kind"] == "port" and "GIL" in cpu["sample"]
+    assert cpu["per_thread_Mpx_s"] == round(cpu["value"] / cpu["cores"], 3)
+
+
+def test_split_predictions_report_every_model():
+    """For N > 1 the bench line carries every balance model's prediction of
+    the split it ran; each model's own split is the one it rates balanced."""
+    import bench
+    from xcube_resampling_amd.sharding import BALANCE_MODELS, band_splits, split_predictions
+
+    _, _, plan, _, _ = bench.workload(4096, 512)
+    for m in BALANCE_MODELS:
+        cuts = band_splits(plan, 8, m)
+        pred = split_predictions(plan, cuts)
+        assert set(pred) == set(BALANCE_MODELS)
+        assert pred[m]["max_over_mean"] < 1.01
+        assert abs(sum(pred[m]["relative"]) - 8) < 1e-3
 
 
 def test_pmc_traffic_reduce(tmp_path):

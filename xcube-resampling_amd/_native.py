@@ -31,6 +31,7 @@ XRS_EFLAG_INDEX = 1
 XRS_EFLAG_BAND = 2
 XRS_EFLAG_NAN_TO_INT = 4
 XRS_EFLAG_INF_TO_INT = 8
+XRS_EFLAG_STATE = 16
 
 INTERP_CODES = {"nearest": 0, "bilinear": 1, "triangular": 2}
 
@@ -95,13 +96,14 @@ _SIGNATURES = {
                                _c_ptr, _c_ptr, _c_ptr, _c_ptr]),
     "xrs_rectify_ij": (_c_int, [_c_ptr, _c_ptr, _c_i64, _c_i64, _c_i64, _c_ptr, _c_i64, _c_i64,
                                 _c_ptr, _c_i64, _c_i64, _c_i64, _c_dbl, _c_dbl, _c_dbl,
-                                _c_ptr, _c_ptr, _c_ptr]),
+                                _c_ptr, _c_ptr, _c_ptr, _c_ptr]),
     "xrs_rectify_tiles": (_c_int, [_c_ptr, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64,
                                    _c_i64, _c_i64, _c_i64, _c_dbl, _c_dbl, _c_dbl, _c_dbl,
                                    _c_dbl, _c_int, _c_ptr, _c_ptr, _c_ptr]),
     "xrs_testing_set": (_c_i64, [_c_int, _c_i64]),
     "xrs_rectify_var": (_c_int, [_c_ptr, _c_i64, _c_i64, _c_i64, _c_ptr, _c_int, _c_i64, _c_i64,
-                                 _c_i64, _c_i64, _c_i64, _c_ptr, _c_i64, _c_int, _c_dbl, _c_ptr]),
+                                 _c_i64, _c_i64, _c_i64, _c_ptr, _c_i64, _c_int, _c_dbl, _c_ptr,
+                                 _c_ptr]),
     "xrs_transform": (_c_int, [_c_ptr, _c_ptr, _c_i64, _c_i64, _c_int, _c_ptr, _c_int, _c_ptr,
                                _c_ptr, _c_ptr]),
     "xrs_reproject_proj": (_c_int, [

@@ -66,11 +66,20 @@ class CRS:
     # ---- pyproj-like API ------------------------------------------------
     @property
     def is_geographic(self) -> bool:
-        return self.kind == "geographic"
+        # a rotated-pole grid is a derived geographic CRS (pyproj: is_geographic)
+        return self.kind in ("geographic", "rotated")
 
     @property
     def is_projected(self) -> bool:
         return not self.is_geographic
+
+    @property
+    def type_name(self) -> str:
+        """pyproj's CRS.type_name for the kinds the engine knows (the
+        reference's tests and dataset.py pick grid mappings by it)."""
+        if self.kind == "rotated":
+            return "Derived Geographic 2D CRS"
+        return "Geographic 2D CRS" if self.is_geographic else "Projected CRS"
 
     @property
     def srs(self) -> str:
@@ -170,6 +179,10 @@ class CRS:
             return _projected_from_cf(attrs)
         if gm_name == "latitude_longitude":
             return _REGISTRY["EPSG:4326"]
+        if gm_name == "rotated_latitude_longitude":
+            return rotated_pole_crs(float(attrs["grid_north_pole_latitude"]),
+                                    float(attrs["grid_north_pole_longitude"]),
+                                    float(attrs.get("north_pole_grid_longitude", 0.0)))
         if gm_name == "mercator" and float(attrs.get("semi_major_axis", _WGS84_A)) == _WGS84_A \
                 and float(attrs.get("inverse_flattening", 0.0)) == 0.0:
             return _REGISTRY["EPSG:3857"]
@@ -299,6 +312,18 @@ def _projected_from_cf(attrs: dict) -> CRS:
         return _REGISTRY["EPSG:3035"]
     return CRS("CF", "laea", attrs.get("projected_crs_name", "Lambert Azimuthal Equal Area"),
                "laea", "en", dict(attrs), params)
+
+def rotated_pole_crs(pole_lat: float, pole_lon: float, pole_grid_lon: float = 0.0) -> CRS:
+    """A CF rotated latitude-longitude grid (``rotated_latitude_longitude``,
+    PROJ ``ob_tran``): recognised for grid-mapping discovery (cfconv.py:66-212
+    assigns rotated coordinates to it); transformations to or from it raise
+    ``NotImplementedError`` (no rotated-pole grid is on the hot path)."""
+    cf = dict(grid_mapping_name="rotated_latitude_longitude",
+              grid_north_pole_latitude=pole_lat, grid_north_pole_longitude=pole_lon,
+              north_pole_grid_longitude=pole_grid_lon)
+    return CRS("CF", "rotated", "Rotated pole (WGS 84)", "rotated", "lonlat", cf,
+               ("WGS 84", pole_lat, pole_lon, pole_grid_lon))
+
 
 CRS_WGS84 = _REGISTRY["EPSG:4326"]
 CRS_CRS84 = _REGISTRY["OGC:CRS84"]
@@ -464,6 +489,10 @@ class Transformer:
             self._separable = True
             self._step_crs = []
             return
+        if "rotated" in (crs_from.kind, crs_to.kind):
+            raise NotImplementedError(
+                f"transformations to or from a rotated-pole grid are not supported "
+                f"({crs_from!r} -> {crs_to!r})")
         steps = []
         self._step_crs = []   # (crs, inverse) per step: the device pipeline (xrs_transform)
         if not crs_from.is_geographic:

@@ -293,7 +293,18 @@ struct RectArgs {
                                // offsets and 24-bit multiplies
   uint32_t* keys;              // (dst_h, dst_w) claim keys, 0xFFFFFFFF = free
   double* ij;                  // (2, dst_h, dst_w) output
+  int32_t* err_flags;          // XRS_EFLAG_STATE: an inconsistent record / key was skipped
 };
+
+// A tile record the claim and resolve passes can address without leaving the
+// target, source or key rasters (records come from xrs_rectify_tiles or the
+// host; anything else is skipped and reported, never dereferenced).
+__device__ inline bool tile_ok(const RectArgs& a, const TileInfo& ti) {
+  return ti.r0 >= 0 && ti.c0 >= 0 && ti.th >= 1 && ti.tw >= 1 &&
+         (int64_t)ti.r0 + ti.th <= a.dst_h && (int64_t)ti.c0 + ti.tw <= a.dst_w &&
+         (ti.si0 < 0 || (ti.sj0 >= 0 && ti.swin >= 0 && ti.shin >= 0 &&
+                         (int64_t)ti.si0 + ti.swin <= a.w && (int64_t)ti.sj0 + ti.shin <= a.h));
+}
 
 struct Quad {          // corners p0 (qj, qi), p1 (qj, qi+1), p2 (qj+1, qi), p3 (qj+1, qi+1)
   double x0, y0, x1, y1, x2, y2, x3, y3;
@@ -642,6 +653,10 @@ rectify_claim_kernel(RectArgs a) {
     }
     lo = __builtin_amdgcn_readfirstlane((int32_t)lo);   // wave-uniform
     const TileInfo ti = a.tiles[lo];
+    if (!tile_ok(a, ti) || ti.si0 < 0) {   // wave-uniform
+      if (lane == 0) atomicOr(a.err_flags, XRS_EFLAG_STATE);
+      continue;
+    }
     const int32_t nq_i = ti.swin - 1, nq_j = ti.shin - 1;
     const int32_t ncx = (nq_i + kStripW - 1) / kStripW;
     const int32_t cc = (int32_t)(c - offs[lo]);
@@ -836,6 +851,10 @@ rectify_resolve_kernel(RectArgs a) {
     const int64_t t = it / bands;
     const int32_t rb = (int32_t)(it - t * bands) * kResolveRows;
     const TileInfo ti = a.tiles[t];
+    if (!tile_ok(a, ti)) {   // block-uniform
+      if (threadIdx.x == 0) atomicOr(a.err_flags, XRS_EFLAG_STATE);
+      continue;
+    }
     if (rb >= ti.th) continue;
     const int32_t nr = min(kResolveRows, ti.th - rb);
     for (int32_t di = threadIdx.x; di < ti.tw; di += kThreads) {
@@ -853,6 +872,11 @@ rectify_resolve_kernel(RectArgs a) {
           int64_t j = (int64_t)((double)key[r] * inv_w);
           int64_t i = (int64_t)key[r] - j * a.w;
           if (i < 0) { --j; i += a.w; } else if (i >= a.w) { ++j; i -= a.w; }
+          if (j < 0 || j > a.h - 2 || i < 0 || i > a.w - 2) {   // not a quad's key
+            atomicOr(a.err_flags, XRS_EFLAG_STATE);
+            key[r] = 0xFFFFFFFFu;
+            continue;
+          }
           qj[r] = j;
           qi[r] = i;
           Q[r] = load_quad(a, j, i);
@@ -898,13 +922,21 @@ __global__ void __launch_bounds__(kThreads)
 rectify_var_kernel(const double* __restrict__ ij, int64_t ij_sn, int64_t dst_h, int64_t dst_w,
                    const T* __restrict__ src, int64_t n, int64_t src_h, int64_t src_w,
                    int64_t src_sn, int64_t src_sy, T* __restrict__ dst, int64_t dst_sn,
-                   double fill) {
+                   double fill, int32_t* err_flags) {
   const int64_t np = dst_h * dst_w;
   const T tfill = Conv<T>::from_f64(fill);
+  bool bad = false;
   for (int64_t p = (int64_t)blockIdx.x * kThreads + threadIdx.x; p < np;
        p += (int64_t)gridDim.x * kThreads) {
     const double fi = ij[p], fj = ij[ij_sn + p];
     if (fi != fi || fj != fj) {
+      for (int64_t s = 0; s < n; ++s) dst[s * dst_sn + p] = tfill;
+      continue;
+    }
+    // K5 positions lie inside the source (src_i_min + src_i <= w - 1,
+    // rectify.py:574-576); anything else is reported, never dereferenced
+    if (!(fi >= 0.0 && fi < (double)src_w && fj >= 0.0 && fj < (double)src_h)) {
+      bad = true;
       for (int64_t s = 0; s < n; ++s) dst[s * dst_sn + p] = tfill;
       continue;
     }
@@ -939,6 +971,7 @@ rectify_var_kernel(const double* __restrict__ ij, int64_t ij_sn, int64_t dst_h, 
       dst[s * dst_sn + p] = Conv<T>::from_f64(val);
     }
   }
+  if (bad) atomicOr(err_flags, XRS_EFLAG_STATE);
 }
 
 // ---- per-tile records + chunk offsets from the K4 accumulators ---------------
@@ -1060,9 +1093,9 @@ extern "C" int xrs_rectify_ij(const double* x, const double* y, int64_t h, int64
                               const int64_t* chunk_offsets, int64_t max_chunks,
                               int64_t dst_h, int64_t dst_w, double x_scale,
                               double y_scale, double uv_delta, uint32_t* keys, double* ij,
-                              void* stream) {
+                              int32_t* err_flags, void* stream) {
   using namespace xrs;
-  if (!x || !y || !tiles || !keys || !ij || h < 2 || w < 2 || sy < w || ntiles < 1 ||
+  if (!x || !y || !tiles || !keys || !ij || !err_flags || h < 2 || w < 2 || sy < w || ntiles < 1 ||
       dst_h < 1 || dst_w < 1 || h * w >= (int64_t)UINT32_MAX || !chunk_offsets || max_chunks < 0 ||
       dst_h > INT32_MAX || dst_w > INT32_MAX) {
     xrs_set_error("xrs_rectify_ij: invalid argument");
@@ -1073,7 +1106,7 @@ extern "C" int xrs_rectify_ij(const double* x, const double* y, int64_t h, int64
   a.tiles = static_cast<const TileInfo*>(tiles); a.ntiles = ntiles;
   a.chunk_offs = chunk_offsets;
   a.dst_h = dst_h; a.dst_w = dst_w; a.x_scale = x_scale; a.y_scale = y_scale;
-  a.uv_delta = uv_delta; a.keys = keys; a.ij = ij;
+  a.uv_delta = uv_delta; a.keys = keys; a.ij = ij; a.err_flags = err_flags;
   a.inv_x = 1.0 / x_scale; a.inv_y = 1.0 / y_scale;
   // tests: xrs_testing_set(XRS_TESTING_RECTIFY_EXACT, 1) takes the exact
   // divisions for every decision
@@ -1107,14 +1140,14 @@ extern "C" int xrs_rectify_var(const double* ij, int64_t ij_sn, int64_t dst_h, i
                                const void* src,
                                int src_dtype, int64_t n, int64_t src_h, int64_t src_w,
                                int64_t src_sn, int64_t src_sy, void* dst, int64_t dst_sn,
-                               int interp, double fill, void* stream) {
+                               int interp, double fill, int32_t* err_flags, void* stream) {
   using namespace xrs;
   if (interp != XRS_INTERP_NEAREST && interp != XRS_INTERP_BILINEAR &&
       interp != XRS_INTERP_TRIANGULAR) {
     xrs_set_error("interp_methods must be one of 0, 1, 'nearest', 'bilinear', 'triangular'");
     return XRS_ERR_NOTIMPL;
   }
-  if (!ij || !src || !dst || dst_h < 1 || dst_w < 1 || n < 1 || src_h < 1 || src_w < 1 ||
+  if (!ij || !src || !dst || !err_flags || dst_h < 1 || dst_w < 1 || n < 1 || src_h < 1 || src_w < 1 ||
       src_sy < src_w || dst_sn < dst_h * dst_w || ij_sn < dst_h * dst_w) {
     xrs_set_error("xrs_rectify_var: invalid argument");
     return XRS_ERR_ARG;
@@ -1127,13 +1160,13 @@ extern "C" int xrs_rectify_var(const double* ij, int64_t ij_sn, int64_t dst_h, i
     T* d = static_cast<T*>(dst);
     if (interp == XRS_INTERP_NEAREST)
       hipLaunchKernelGGL((rectify_var_kernel<T, XRS_INTERP_NEAREST>), dim3(nb), dim3(kThreads),
-                         0, st, ij, ij_sn, dst_h, dst_w, s, n, src_h, src_w, src_sn, src_sy, d, dst_sn, fill);
+                         0, st, ij, ij_sn, dst_h, dst_w, s, n, src_h, src_w, src_sn, src_sy, d, dst_sn, fill, err_flags);
     else if (interp == XRS_INTERP_TRIANGULAR)
       hipLaunchKernelGGL((rectify_var_kernel<T, XRS_INTERP_TRIANGULAR>), dim3(nb), dim3(kThreads),
-                         0, st, ij, ij_sn, dst_h, dst_w, s, n, src_h, src_w, src_sn, src_sy, d, dst_sn, fill);
+                         0, st, ij, ij_sn, dst_h, dst_w, s, n, src_h, src_w, src_sn, src_sy, d, dst_sn, fill, err_flags);
     else
       hipLaunchKernelGGL((rectify_var_kernel<T, XRS_INTERP_BILINEAR>), dim3(nb), dim3(kThreads),
-                         0, st, ij, ij_sn, dst_h, dst_w, s, n, src_h, src_w, src_sn, src_sy, d, dst_sn, fill);
+                         0, st, ij, ij_sn, dst_h, dst_w, s, n, src_h, src_w, src_sn, src_sy, d, dst_sn, fill, err_flags);
     XRS_HIP_CHECK(hipGetLastError());
     return XRS_OK;
   });

@@ -54,8 +54,17 @@ def _get_dataset_chunks(dataset) -> dict:
     return out
 
 
+def _is_potential_coord_var(dataset, bounds_var_names, var_name) -> bool:
+    """cfconv.py:299-305."""
+    if var_name in dataset:
+        return dataset[var_name].ndim in (1, 2) and var_name not in bounds_var_names
+    return False
+
+
 def _find_potential_coord_vars(dataset) -> list:
-    """cfconv.py:256-295."""
+    """cfconv.py:254-296: 1-D / 2-D variables that are not bounds variables
+    (CF ``bounds`` attribute or a ``<name>_bnds`` / ``<name>_bounds`` name),
+    those of the global ``coordinates`` attribute first."""
     bounds_vars = set()
     for k in dataset.variables:
         var = dataset[k]
@@ -67,12 +76,12 @@ def _find_potential_coord_vars(dataset) -> list:
             bounds_vars.add(k)
     out = []
     coordinates = dataset.attrs.get("coordinates")
-    names = (coordinates.split() if coordinates else []) + list(dataset.variables)
-    for name in names:
-        if name in out or name not in dataset:
-            continue
-        var = dataset[name]
-        if var.ndim in (1, 2) and name not in bounds_vars:
+    if coordinates is not None:
+        for name in coordinates.split():
+            if _is_potential_coord_var(dataset, bounds_vars, name):
+                out.append(name)
+    for name in dataset.variables:
+        if name not in out and _is_potential_coord_var(dataset, bounds_vars, name):
             out.append(name)
     return out
 
@@ -95,8 +104,10 @@ def _complement(coords: _GridCoords, gm_name, missing_crs, proxies: dict):
 
 
 def get_dataset_grid_mapping_proxies(dataset, *, missing_latitude_longitude_crs=None,
+                                     missing_rotated_latitude_longitude_crs=None,
                                      missing_projected_crs=None, emit_warnings=False) -> dict:
-    """cfconv.py:66-212 (rotated lat/lon grids are not supported by the engine)."""
+    """cfconv.py:66-212.  Rotated-pole grids are discovered (their CRS is
+    recognised from the CF attributes) but cannot be resampled."""
     proxies: dict = {}
     for var in dataset.variables.values():
         gm_var_name = var.attrs.get("grid_mapping")
@@ -115,32 +126,35 @@ def get_dataset_grid_mapping_proxies(dataset, *, missing_latitude_longitude_crs=
         if gmp is not None:
             proxies[None] = gmp
 
-    latlon, projected = _GridCoords(), _GridCoords()
+    latlon, rotated, projected = _GridCoords(), _GridCoords(), _GridCoords()
     candidates = _find_potential_coord_vars(dataset)
+    by_standard_name = ((latlon, "longitude", "latitude"),
+                        (rotated, "grid_longitude", "grid_latitude"),
+                        (projected, "projection_x_coordinate", "projection_y_coordinate"))
     for name in candidates:
         var = dataset[name]
         sn = var.attrs.get("standard_name")
-        if latlon.x is None and sn == "longitude":
-            latlon.x = var
-        if latlon.y is None and sn == "latitude":
-            latlon.y = var
-        if projected.x is None and sn == "projection_x_coordinate":
-            projected.x = var
-        if projected.y is None and sn == "projection_y_coordinate":
-            projected.y = var
+        for coords, xn, yn in by_standard_name:
+            if coords.x is None and sn == xn:
+                coords.x = var
+            if coords.y is None and sn == yn:
+                coords.y = var
+    by_name = ((latlon, ("lon", "longitude"), ("lat", "latitude")),
+               (rotated, ("rlon", "rlongitude"), ("rlat", "rlatitude")),
+               (projected, ("x", "xc", "transformed_x"), ("y", "yc", "transformed_y")))
     for name in candidates:
         var = dataset[name]
-        if latlon.x is None and name in ("lon", "longitude"):
-            latlon.x = var
-        if latlon.y is None and name in ("lat", "latitude"):
-            latlon.y = var
-        if projected.x is None and name in ("x", "xc", "transformed_x"):
-            projected.x = var
-        if projected.y is None and name in ("y", "yc", "transformed_y"):
-            projected.y = var
+        for coords, xns, yns in by_name:
+            if coords.x is None and name in xns:
+                coords.x = var
+            if coords.y is None and name in yns:
+                coords.y = var
     for gmp in proxies.values():
-        gmp.coords = latlon if gmp.name == "latitude_longitude" else projected
+        gmp.coords = (latlon if gmp.name == "latitude_longitude" else
+                      rotated if gmp.name == "rotated_latitude_longitude" else projected)
     _complement(latlon, "latitude_longitude", missing_latitude_longitude_crs or CRS_WGS84, proxies)
+    _complement(rotated, "rotated_latitude_longitude", missing_rotated_latitude_longitude_crs,
+                proxies)
     _complement(projected, None, missing_projected_crs, proxies)
 
     complete = {}
@@ -173,6 +187,7 @@ def new_grid_mapping_from_dataset(dataset, *, crs=None, tile_size=None, prefer_c
     prefer_crs = normalize_crs(prefer_crs) if prefer_crs is not None else crs
     proxies = get_dataset_grid_mapping_proxies(
         dataset, emit_warnings=emit_warnings, missing_projected_crs=crs,
+        missing_rotated_latitude_longitude_crs=crs,
         missing_latitude_longitude_crs=crs).values()
     gms = [new_grid_mapping_from_coords(x_coords=g.coords.x, y_coords=g.coords.y, crs=g.crs,
                                         tile_size=tile_size or g.tile_size, tolerance=tolerance)

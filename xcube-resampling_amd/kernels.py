@@ -39,6 +39,10 @@ class ErrorFlags:
             raise ValueError("cannot convert float NaN to integer")
         if bits & _native.XRS_EFLAG_INF_TO_INT:
             raise OverflowError("cannot convert float infinity to integer")
+        if bits & _native.XRS_EFLAG_STATE:
+            raise _native.NativeLibraryError(
+                f"{what}: inconsistent rectify state (a tile record, claim key or source "
+                f"position outside its raster was skipped)")
 
 
 def reproject(src, plan, interp: str, fill: float, out_dtype=None, rows=None, out=None,
@@ -265,12 +269,15 @@ def strip_counts(swin, shin):
 
 
 def rectify_ij(x_image, y_image, tiles: np.ndarray, ntiles_x: int, dst_h: int, dst_w: int,
-               x_scale: float, y_scale: float, uv_delta: float, device=None, stream=None):
+               x_scale: float, y_scale: float, uv_delta: float, device=None, stream=None,
+               flags: ErrorFlags | None = None):
     """K5 — per target pixel the fractional source (i, j) (rectify.py:373-576).
 
     tiles: structured array of TILE_INFO_DTYPE (row-major tile order), or
     the (tiles, chunk offsets) device pair of rectify_tiles_device.
     Returns a device tensor (2, dst_h, dst_w) float64 (NaN = no source pixel).
+    An inconsistent tile record or claim key (skipped, never dereferenced)
+    raises; with a caller's ``flags`` the caller checks them (no sync here).
     """
     device = require_device(device)
     x = to_device(x_image, device, np.float64)
@@ -288,19 +295,26 @@ def rectify_ij(x_image, y_image, tiles: np.ndarray, ntiles_x: int, dst_h: int, d
         ntiles, max_chunks = offs.numel() - 1, 0
     keys = torch().empty((dst_h, dst_w), dtype=torch().int32, device=device)
     ij = torch().empty((2, dst_h, dst_w), dtype=torch().float64, device=device)
+    own_flags = flags is None
+    if own_flags:
+        flags = ErrorFlags(device)
     rc = _native.lib().xrs_rectify_ij(ptr(x), ptr(y), h, w, x.stride(0), ptr(t_dev), ntiles,
                                       ntiles_x, ptr(offs), max_chunks, dst_h, dst_w,
                                       float(x_scale), float(y_scale), float(uv_delta),
-                                      ptr(keys), ptr(ij), stream_handle(device, stream))
+                                      ptr(keys), ptr(ij), flags.ptr, stream_handle(device, stream))
     _native.check(rc, "xrs_rectify_ij")
+    if own_flags:
+        flags.raise_if_set("xrs_rectify_ij")
     return ij
 
 
-def rectify_var(ij, src, interp: str, fill, stream=None, rows=None, out=None):
+def rectify_var(ij, src, interp: str, fill, stream=None, rows=None, out=None,
+                flags: ErrorFlags | None = None):
     """K6 — sample one variable (n, H, W) at the fractional source positions
     `ij` (2, H', W') (rectify.py:605-734).  Returns (n, H', W') in src dtype,
     or with ``rows=(r0, r1)`` the target rows [r0, r1) into ``out`` (n, r1-r0,
-    W') (default: a new tensor)."""
+    W') (default: a new tensor).  Positions outside the source (never made
+    by K5) raise; with a caller's ``flags`` the caller checks them."""
     device = src.device
     code = _native.INTERP_CODES.get(interp)
     if code is None:
@@ -318,11 +332,16 @@ def rectify_var(ij, src, interp: str, fill, stream=None, rows=None, out=None):
             out.stride()[1:] != (dw, 1):
         raise ValueError("out must be (n, rows, W') in the source dtype, rows contiguous")
     ij = ij.contiguous()
+    own_flags = flags is None
+    if own_flags:
+        flags = ErrorFlags(device)
     rc = _native.lib().xrs_rectify_var(
         ptr(ij) + r0 * dw * 8, dh * dw, r1 - r0, dw, ptr(src),
         _native.DTYPE_CODES[_np_dtype(src)], n, h, w, src.stride(0), src.stride(1), ptr(out),
-        out.stride(0), code, float(fill), stream_handle(device, stream))
+        out.stride(0), code, float(fill), flags.ptr, stream_handle(device, stream))
     _native.check(rc, "xrs_rectify_var")
+    if own_flags:
+        flags.raise_if_set("xrs_rectify_var")
     return out
 
 

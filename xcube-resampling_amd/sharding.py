@@ -71,32 +71,20 @@ COST_SRC_ROW_WEIGHT = 0.74
 COST_DUP_ROW_WEIGHT = 0.45
 
 
-def band_splits(plan, world: int, balance: str = "rows", out_itemsize: int = 4) -> list[int]:
-    """Target-row boundaries r_0 = 0 <= r_1 <= ... <= r_world = H of a
-    `world`-way split of one raster at ROW granularity (K1 takes arbitrary
-    row bands: ``xrs_reproject(row_begin, row_end)``; SURVEY §8(e) — whole
-    tile rows give a 3/3/3/3/2/2/2/2 split of config 5's 20 tile rows).
+BALANCE_MODELS = ("rows", "bytes", "cost")
 
-    balance="rows":  equal target rows (equal output bytes and gather work);
-    balance="bytes": equal algorithmic bytes per band (output + the distinct
-                     source rows it reads: at config 5 a target row near 30 N
-                     reads 2.6x the source rows of one near 70 N);
-    balance="cost":  equal measured K1 time: rows + COST_SRC_ROW_WEIGHT x
-                     source rows + COST_DUP_ROW_WEIGHT x rows repeating the
-                     previous row's floor source row (the gather is bound by
-                     target pixels more than by source bytes: equal bytes
-                     over-corrects)."""
+
+def _cumulative_cost(plan, balance: str, out_itemsize: int) -> np.ndarray:
+    """F(r), r = 0..H: predicted cost of target rows [0, r) under one model."""
     h = plan.dst_height
-    if world < 1:
-        raise ValueError(f"invalid world size {world}")
     if balance == "rows":
-        return [balanced_range(h, world, r)[0] for r in range(world)] + [h]
+        return np.arange(h + 1, dtype=np.float64)
     if balance == "bytes":
         row_w, src_w = out_itemsize * plan.dst_width, 4 * plan.source_cols_read()
     elif balance == "cost":
         row_w, src_w = 1.0, COST_SRC_ROW_WEIGHT
     else:
-        raise ValueError(f"balance must be 'rows', 'bytes' or 'cost', was {balance!r}")
+        raise ValueError(f"balance must be one of {BALANCE_MODELS}, was {balance!r}")
     lo, hi = plan.row_source_extent()
     valid = hi >= lo
     # cumulative cost F(r) of target rows [0, r): rows + distinct source rows
@@ -110,9 +98,49 @@ def band_splits(plan, world: int, balance: str = "rows", out_itemsize: int = 4) 
         dup = np.zeros(h, bool)
         dup[1:] = (lo[1:] == lo[:-1]) & valid[1:] & valid[:-1]
         f = f + COST_DUP_ROW_WEIGHT * np.concatenate([[0], np.cumsum(dup)])
+    return f
+
+
+def band_splits(plan, world: int, balance: str = "rows", out_itemsize: int = 4) -> list[int]:
+    """Target-row boundaries r_0 = 0 <= r_1 <= ... <= r_world = H of a
+    `world`-way split of one raster at ROW granularity (K1 takes arbitrary
+    row bands: ``xrs_reproject(row_begin, row_end)``; SURVEY §8(e) — whole
+    tile rows give a 3/3/3/3/2/2/2/2 split of config 5's 20 tile rows).
+
+    balance="rows":  equal target rows (equal output bytes and gather work);
+    balance="bytes": equal algorithmic bytes per band (output + the distinct
+                     source rows it reads: at config 5 a target row near 30 N
+                     reads 2.6x the source rows of one near 70 N) — the
+                     unfitted HBM-bound model, kept as the guard of "cost";
+    balance="cost":  equal predicted K1 time: rows + COST_SRC_ROW_WEIGHT x
+                     source rows + COST_DUP_ROW_WEIGHT x rows repeating the
+                     previous row's floor source row (weights fitted to
+                     one-GPU rehearsals; ``split_predictions`` reports every
+                     model's balance of a split, so a multi-GPU run shows
+                     which one held)."""
+    h = plan.dst_height
+    if world < 1:
+        raise ValueError(f"invalid world size {world}")
+    if balance == "rows":
+        return [balanced_range(h, world, r)[0] for r in range(world)] + [h]
+    f = _cumulative_cost(plan, balance, out_itemsize)
     targets = f[-1] * np.arange(1, world) / world
     cuts = np.searchsorted(f, targets, side="left")
     return [0] + [int(c) for c in cuts] + [h]
+
+
+def split_predictions(plan, cuts: list[int], out_itemsize: int = 4) -> dict:
+    """Per-band cost of the split `cuts` predicted by every balance model,
+    relative to the model's mean over the bands, plus each model's max/mean
+    (a measured per-rank time series is compared against these)."""
+    out = {}
+    for m in BALANCE_MODELS:
+        f = _cumulative_cost(plan, m, out_itemsize)
+        per = np.array([f[b] - f[a] for a, b in zip(cuts[:-1], cuts[1:])], np.float64)
+        mean = per.mean() if per.size and per.mean() > 0 else 1.0
+        out[m] = {"relative": [round(float(x), 4) for x in per / mean],
+                  "max_over_mean": round(float(per.max() / mean), 4) if per.size else 1.0}
+    return out
 
 
 def band_shard(plan, world: int, rank: int, balance: str = "rows",

@@ -317,11 +317,15 @@ def rectify_host(src: np.ndarray, ij, interp: str, fill, device=None,
         else:
             src_rows.append((int(np.floor(blo)), int(np.floor(bhi)) + 2))
     dsrc = empty((n, h, w), src.dtype, device)
+    flags = kernels.ErrorFlags(device)
 
     def launch(b, r0, r1, buf, stream):
-        kernels.rectify_var(ij, dsrc, interp, fill, stream=stream, rows=(r0, r1), out=buf)
+        kernels.rectify_var(ij, dsrc, interp, fill, stream=stream, rows=(r0, r1), out=buf,
+                            flags=flags)
 
-    return band_pipeline(src, dsrc, out, bands, src_rows, launch, device, poison)
+    band_pipeline(src, dsrc, out, bands, src_rows, launch, device, poison)
+    flags.raise_if_set("rectify")
+    return out
 
 
 def affine_host(src: np.ndarray, plan, device=None, band_chunks: int | None = None,
