@@ -347,7 +347,7 @@ def main():
     flags = kernels.ErrorFlags(device)
     benchlib = load_benchlib()
     stream = torch.cuda.current_stream(device)   # the stream the kernels run on
-    copy_gbs = device_copy_rate(benchlib, src, stream)
+    copy_rates = []
 
     def make_step(out, dtype):
         def step():
@@ -373,6 +373,10 @@ def main():
             with torch.cuda.graph(g):
                 step()
             run = g.replay
+        # the same-run device-copy rate, measured back to back with the warm-up
+        # steps: its ~0.1 s of streaming also takes the shader clock to its
+        # loaded level (DVFS: ~30 ms of load from idle), as W steps alone may not
+        copy_rates.append(device_copy_rate(benchlib, src, stream))
         for _ in range(warmup):
             run()
         torch.cuda.synchronize()
@@ -397,6 +401,7 @@ def main():
     ms_per_step, kernel_ms, clocks = timed(make_step(out, out_np), args.steps, args.warmup)
     flags.raise_if_set("bench reproject")
 
+    copy_gbs = copy_rates[0]
     s_read = source_pixels_read(plan, rows) if rows[1] > rows[0] else 0
     out_bytes = (rows[1] - rows[0]) * args.size * np.dtype(out_np).itemsize
     my_bytes = out_bytes + 4 * s_read

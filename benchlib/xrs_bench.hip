@@ -71,6 +71,8 @@ __global__ void __launch_bounds__(256) region_copy_kernel(const float* __restric
                                                           int64_t segw, int64_t band,
                                                           int64_t nsegs, int64_t nwork,
                                                           int order) {
+  extern __shared__ float occupancy_pad[];   // dynamic LDS only limits blocks per CU
+  if (threadIdx.x == 1024) occupancy_pad[0] = 0.0f;   // never true: keeps the allocation
   int64_t w = blockIdx.x;
   if (order == 1) {
     const int64_t xcd = blockIdx.x % 8, i = blockIdx.x / 8;
@@ -102,9 +104,19 @@ __global__ void __launch_bounds__(256) region_copy_kernel(const float* __restric
   }
 }
 
+extern "C" int xrs_bench_region_copy_lds(const void* src, void* dst, int64_t rows, int64_t cols,
+                                         int64_t segw, int64_t band, int rif, int nt, int order,
+                                         int lds_bytes, void* stream);
+
 extern "C" int xrs_bench_region_copy(const void* src, void* dst, int64_t rows, int64_t cols,
                                      int64_t segw, int64_t band, int rif, int nt, int order,
                                      void* stream) {
+  return xrs_bench_region_copy_lds(src, dst, rows, cols, segw, band, rif, nt, order, 0, stream);
+}
+
+extern "C" int xrs_bench_region_copy_lds(const void* src, void* dst, int64_t rows, int64_t cols,
+                                         int64_t segw, int64_t band, int rif, int nt, int order,
+                                         int lds_bytes, void* stream) {
   if (segw % 4 || cols % segw || rows % band || (band * segw / 4) % 64) return -1;
   const int64_t nsegs = cols / segw, nwork = (rows / band) * nsegs;
   const int64_t nb = ((nwork + 7) / 8) * 8;
@@ -112,7 +124,7 @@ extern "C" int xrs_bench_region_copy(const void* src, void* dst, int64_t rows, i
   const float* s = (const float*)src;
   float* d = (float*)dst;
 #define XRS_RC(R, N)                                                                         \
-  hipLaunchKernelGGL((region_copy_kernel<R, N>), dim3((unsigned)nb), dim3(256), 0, st, s, d, \
+  hipLaunchKernelGGL((region_copy_kernel<R, N>), dim3((unsigned)nb), dim3(256), lds_bytes, st, s, d, \
                      cols, segw, band, nsegs, nwork, order)
   if (rif == 1) { if (nt) XRS_RC(1, true); else XRS_RC(1, false); }
   else if (rif == 2) { if (nt) XRS_RC(2, true); else XRS_RC(2, false); }

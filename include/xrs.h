@@ -263,6 +263,23 @@ int xrs_rectify_ij(const double* x, const double* y, int64_t h, int64_t w, int64
                    void* stream);
 
 /* -------------------------------------------------------------------------
+ * xrs_rectify_ij_var — xrs_rectify_ij with the first variable sampled by the
+ * resolve pass itself (xrs_rectify_var's per-pixel sampling, rectify.py:
+ * 605-734, fused into K5b): the variable (n, src_h, src_w) of dtype
+ * src_dtype is written to dst (n, dst_h, dst_w) as xrs_rectify_var would
+ * write it from the ij image.  ij may be NULL when no other variable needs
+ * the positions (the ij image is then never written); else it is written as
+ * by xrs_rectify_ij.  (xrs_rectify_ij's ntiles_x, unused, is omitted.)
+ * ------------------------------------------------------------------------- */
+int xrs_rectify_ij_var(const double* x, const double* y, int64_t h, int64_t w, int64_t sy,
+                       const void* tiles, int64_t ntiles, const int64_t* chunk_offsets,
+                       int64_t max_chunks, int64_t dst_h, int64_t dst_w, double x_scale,
+                       double y_scale, double uv_delta, uint32_t* keys, double* ij,
+                       const void* src, int src_dtype, int64_t n, int64_t src_h, int64_t src_w,
+                       int64_t src_sn, int64_t src_sy, void* dst, int64_t dst_sn, int interp,
+                       double fill, int32_t* err_flags, void* stream);
+
+/* -------------------------------------------------------------------------
  * xrs_rectify_tiles — the host-side tiling of _compute_target_source_ij
  * (rectify.py:312-419: per target tile its source ij bbox, via
  * ij_bboxes_from_xy_bboxes base.py:565-629 + bboxes.py:90-106, the source

@@ -61,8 +61,10 @@ def target_tiles(size, tile_size):
 
 
 def compute_target_source_ij(src_x, src_y, size, tile_size, xy_bbox, xy_res, j_up=False,
-                             uv_delta=1e-3, threads=1):
-    """rectify.py:312-419 for a target grid (size, tile_size, xy_bbox, xy_res)."""
+                             uv_delta=1e-3, threads=1, tile_ids=None):
+    """rectify.py:312-419 for a target grid (size, tile_size, xy_bbox, xy_res);
+    ``tile_ids``: only those target tiles (raster order), the others NaN — a
+    dask worker's share of the tiles (rectify.py:347-370)."""
     w, h = size
     tw, th = tile_size
     x_min, y_min, x_max, y_max = xy_bbox
@@ -91,15 +93,19 @@ def compute_target_source_ij(src_x, src_y, size, tile_size, xy_bbox, xy_res, j_u
         return k, blk
 
     tiles = list(enumerate(target_tiles(size, tile_size)))
+    if tile_ids is not None:
+        keep = set(int(t) for t in tile_ids)
+        tiles = [kt for kt in tiles if kt[0] in keep]
     with ThreadPoolExecutor(max_workers=threads) as ex:
         for k, blk in ex.map(block, tiles):
-            r0, r1, c0, c1 = tiles[k][1]
+            r0, r1, c0, c1 = dict(tiles)[k]
             out[:, r0:r1, c0:c1] = blk
     return out, ij_bboxes
 
 
-def compute_var_image(ij, var, fill_value, interp, tile_size, threads=1):
-    """rectify.py:579-635: per target tile, source sub-window + sequential loop."""
+def compute_var_image(ij, var, fill_value, interp, tile_size, threads=1, tile_ids=None):
+    """rectify.py:579-635: per target tile, source sub-window + sequential loop
+    (``tile_ids``: only those tiles, the others fill)."""
     codes = {"nearest": 0, "bilinear": 1, "triangular": 2}
     if interp not in codes:
         raise NotImplementedError(
@@ -130,8 +136,11 @@ def compute_var_image(ij, var, fill_value, interp, tile_size, threads=1):
                                            _p(written))
         return t, (vals, written.astype(bool))
 
+    tl = target_tiles((w, h), tile_size)
+    if tile_ids is not None:
+        tl = [tl[int(t)] for t in tile_ids]
     with ThreadPoolExecutor(max_workers=threads) as ex:
-        for (r0, r1, c0, c1), res in ex.map(block, target_tiles((w, h), tile_size)):
+        for (r0, r1, c0, c1), res in ex.map(block, tl):
             if res is None:
                 continue
             vals, written = res

@@ -201,22 +201,25 @@ def config2u(args):
     e_ms, wall = _timed(end_to_end, max(3, args.steps // 4), 1)
     flags.raise_if_set("config 2u")
     covered = int(torch.isfinite(out).sum().item())
-    # CPU: the numpy restatement of the per-pixel transformation of 2048^2 tiles
-    # (the reference's _transform_gridpoints, its dominant per-tile cost)
-    xx, yy = np.meshgrid(plan.grid_x[:2048], plan.grid_y[:2048])
-    cpu_v, px, dt = _cpu_loop(lambda: (tr.transform(xx, yy), xx.size)[1], args.cpu_seconds, 0)
+    # CPU: the numpy restatement of the per-pixel transformation, one 512^2
+    # block per task on a pool over all cores (the reference's
+    # _transform_gridpoints per dask block, its dominant per-block cost)
+    xx, yy = np.meshgrid(plan.grid_x[:512], plan.grid_y[:512])
+    cpu_v, px, dt, cores = _cpu_pool(lambda: (tr.transform(xx, yy), xx.size)[1],
+                                     args.cpu_seconds)
     # algorithmic bytes of the end-to-end step: tables written + read (32 B/px),
     # f64 out, f32 source reads (<= the source once)
     alg = 16 * size * size + 16 * size * size + 8 * size * size + 4 * size * size
     _line("2u", "reproject bilinear 8192x8192 f32 UTM 32N (EPSG:32632) -> LAEA Europe "
                 "(EPSG:3035) 30 m, 2048^2 tiles, f64 out; per-pixel transform on the device "
-                "(xrs_transform: tmerc inverse + laea forward) then K1 on 2-D tables, end to end",
+                "(xrs_transform: laea inverse + tmerc forward) then K1 on 2-D tables, end to end",
           size * size, e_ms, wall, alg,
           f"transform_kernel<true> {t_ms:.3f} ms + gather K1 (2-D tables) {k_ms:.3f} ms",
-          dict(value=round(cpu_v, 2), unit="Mpixels/s", cores=1, kind="port",
-               sample=f"numpy restatement of the per-pixel UTM -> LAEA transform "
-                      f"(projections.py) over {px // xx.size} 2048^2 tiles in {dt:.1f} s, "
-                      "one thread (the transform alone; the block gather is not included)"),
+          dict(value=round(cpu_v, 2), unit="Mpixels/s", cores=cores, kind="port",
+               sample=f"numpy restatement of the per-pixel LAEA -> UTM transform "
+                      f"(projections.py) over {px // xx.size} 512^2 blocks in {dt:.1f} s on "
+                      f"{cores} threads (the transform alone; the block gather is not "
+                      "included; numpy's ufuncs hold the GIL between calls)"),
           {"transform_ms": round(t_ms, 4), "k1_ms": round(k_ms, 4), "covered_px": covered,
            "transform_gpts_s": round(size * size / (t_ms / 1e3) / 1e9, 2)})
 
@@ -235,8 +238,8 @@ def config2u(args):
                       "(EPSG:3035) 30 m, 2048^2 tiles, f64 out; transformation fused into the "
                       "gather (xrs_reproject_proj), bit-identical to the tables path",
           size * size, f_ms, f_wall, 8 * size * size + 4 * size * size,
-          "gather_proj_kernel<TMERC_INV, LAEA_FWD>",
-          dict(value=round(cpu_v, 2), unit="Mpixels/s", cores=1, kind="port",
+          "gather_proj_kernel<LAEA_INV, TMERC_FWD>",
+          dict(value=round(cpu_v, 2), unit="Mpixels/s", cores=cores, kind="port",
                sample="as the 2u line"), {"covered_px": covered})
 
 
@@ -335,11 +338,17 @@ def config4(args):
                           args.steps, args.warmup)
         lines[interp] = k6_ms
 
-    def pipeline(interp):   # K4 -> device tiling -> K5 -> K6, no host round trip
+    def separate(interp):   # K4 -> device tiling -> K5 -> K6, no host round trip
         t = R._device_tiles(sgm, tgm, xy)
         ij_ = kernels.rectify_ij(xy[0], xy[1], t, ntx, tgm.height, tgm.width, tgm.x_res,
                                  dst_y_scale, 1e-3, flags=flags)
         return kernels.rectify_var(ij_, src, interp, float("nan"), flags=flags)
+
+    def pipeline(interp):   # rectify_dataset's single-variable path: K6 inside K5b
+        t = R._device_tiles(sgm, tgm, xy)
+        return kernels.rectify_ij_var(xy[0], xy[1], t, tgm.height, tgm.width, tgm.x_res,
+                                      dst_y_scale, 1e-3, src, interp, float("nan"),
+                                      keep_ij=False, flags=flags)[1]
 
     # the device tiling reproduces the host tiling byte for byte
     t_dev, offs = R._device_tiles(sgm, tgm, xy)
@@ -347,12 +356,16 @@ def config4(args):
     assert torch.equal(torch.nan_to_num(pipeline("nearest"), 12345.0),
                        torch.nan_to_num(kernels.rectify_var(ij, src, "nearest", float("nan")),
                                         12345.0)), "device-tiled pipeline"
+    for interp in ("nearest", "bilinear"):
+        assert torch.equal(torch.nan_to_num(pipeline(interp), 12345.0),
+                           torch.nan_to_num(separate(interp), 12345.0)), "fused K5+K6"
 
 
     npx = tgm.width * tgm.height
     S = w * h
     for interp in ("nearest", "bilinear"):
         ms, wall = _timed(lambda: pipeline(interp), max(3, args.steps // 4), 1)
+        sep_ms, _ = _timed(lambda: separate(interp), max(3, args.steps // 4), 1)
         cores = len(os.sched_getaffinity(0))
         # bounded CPU sample: a 1000x1200 sub-swath rectified onto its own bbox
         sub = (slice(0, 1200), slice(0, 1000))
@@ -372,7 +385,8 @@ def config4(args):
         cpu_v, px, dt = _cpu_loop(cpu_once, args.cpu_seconds, 0)
         _line(4, f"rectify {interp}: 4000x4800 jittered swath (f64 lon/lat, f32 var) -> "
                  f"{tgm.width}x{tgm.height} EPSG:4326 res 0.0027, 512^2 tiles "
-                 "(K4 bbox + device tiling + K5 + K6, end to end, coordinates resident in HBM)",
+                 "(K4 bbox + device tiling + K5 with K6 fused, end to end, coordinates "
+                 "resident in HBM)",
               npx, ms, wall, 16 * S + 4 * S + 4 * npx,
               f"K5 rectify_claim+resolve {k5_ms:.3f} ms, K6 {lines[interp]:.3f} ms",
               dict(value=round(cpu_v, 2), unit="Mpixels/s", cores=cores, kind="port",
@@ -380,7 +394,7 @@ def config4(args):
                           f"{ssz[0]}x{ssz[1]} in {dt:.1f} s (C restatement of the numba "
                           "kernels, tiles on a thread pool)"),
               {"covered_px": covered, "k5_ms": round(k5_ms, 4),
-               "k6_ms": round(lines[interp], 4)})
+               "k6_ms": round(lines[interp], 4), "unfused_ms": round(sep_ms, 4)})
     flags.raise_if_set("config 4")
 
 

@@ -95,6 +95,32 @@ def main():
         torch.cuda.synchronize()
         assert torch.equal(a, b)
 
+    # K1's shape with fewer blocks resident per CU (dynamic LDS as the limiter)
+    lib.xrs_bench_region_copy_lds.argtypes = [ctypes.c_void_p, ctypes.c_void_p] + \
+        [ctypes.c_int64] * 4 + [ctypes.c_int] * 4 + [ctypes.c_void_p]
+    occ = [(c, bpc) for c in [(512, 32, 4, 1, 1), (1024, 8, 4, 1, 1), (1024, 32, 4, 1, 1)]
+           for bpc in (1, 2, 3, 4, 6, 8)]
+    for p in ((1, 2) if "occupancy" in sections else ()):
+        for c, bpc in occ:
+            lds = (160 * 1024) // bpc - 1024 if bpc < 8 else 0
+
+            def oc():
+                if lib.xrs_bench_region_copy_lds(a.data_ptr(), b.data_ptr(), 40960, 40960, *c,
+                                                 lds, sh):
+                    raise RuntimeError(f"region copy {c} failed")
+            for _ in range(3):
+                oc()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            for _ in range(20):
+                oc()
+            e1.record(st)
+            torch.cuda.synchronize()
+            ms = e0.elapsed_time(e1) / 20
+            print(json.dumps({"occupancy": dict(zip(("segw", "band", "rif", "nt", "order"), c)),
+                              "blocks_per_cu": bpc, "pass": p, "ms": round(ms, 4),
+                              "GBs": round(2 * nbytes / ms / 1e6, 1)}), flush=True)
+
     # persistent row-walking copies: (float4 per thread per item, blocks, nt)
     lib.xrs_bench_persistent_copy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
                                               ctypes.c_int64, ctypes.c_int, ctypes.c_int,

@@ -1,7 +1,8 @@
 """Config-4 rectify kernels timed in isolation (K4 + device tiles, K5 claim +
 resolve, K6 nearest): the workload of scripts/bench_configs.py config4, for
-rocprofv3 --kernel-trace --stats runs of kernel variants.
-    python scripts/time_rectify.py [--reps N]"""
+rocprofv3 --kernel-trace --stats runs of kernel variants.  --fused samples the
+variable inside K5's resolve pass (xrs_rectify_ij_var, no ij image written).
+    python scripts/time_rectify.py [--reps N] [--fused]"""
 
 from __future__ import annotations
 
@@ -17,6 +18,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--fused", action="store_true")
     args = ap.parse_args()
     import torch
 
@@ -42,18 +44,25 @@ def main():
     src = torch.from_numpy(var).cuda()
     ntx = len(range(0, tgm.width, tgm.tile_width))
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    flags = kernels.ErrorFlags(src.device)   # checked once, after the timed loop
     for r in range(args.reps + 2):
         if r == 2:
             torch.cuda.synchronize()
             ev[0].record()
         t = R._device_tiles(sgm, tgm, xy)
-        ij = kernels.rectify_ij(xy[0], xy[1], t, ntx, tgm.height, tgm.width, tgm.x_res,
-                                -tgm.y_res, 1e-3)
-        out = kernels.rectify_var(ij, src, "nearest", float("nan"))
+        if args.fused:
+            _, out = kernels.rectify_ij_var(xy[0], xy[1], t, tgm.height, tgm.width, tgm.x_res,
+                                            -tgm.y_res, 1e-3, src, "nearest", float("nan"),
+                                            keep_ij=False, flags=flags)
+        else:
+            ij = kernels.rectify_ij(xy[0], xy[1], t, ntx, tgm.height, tgm.width, tgm.x_res,
+                                    -tgm.y_res, 1e-3, flags=flags)
+            out = kernels.rectify_var(ij, src, "nearest", float("nan"), flags=flags)
     ev[1].record()
     torch.cuda.synchronize()
+    flags.raise_if_set("time_rectify")
     print(f"{os.environ.get('XRS_LIBRARY', 'libxrs.so')}: {ev[0].elapsed_time(ev[1]) / args.reps:.3f} "
-          f"ms per K4+K5+K6, covered {int(torch.isfinite(out).sum())} px", flush=True)
+          f"ms per K4+K5+K6{' (fused)' if args.fused else ''}, covered {int(torch.isfinite(out).sum())} px", flush=True)
 
 
 if __name__ == "__main__":

@@ -286,6 +286,84 @@ def test_device_tiling_matches_host_tiling(j_up, tile):
     assert_bitwise_equal(b.cpu().numpy(), a.cpu().numpy(), "device vs host tiles")
 
 
+@pytest.mark.parametrize("dtype,interp,n,keep_ij", [
+    (np.float32, "nearest", 1, False), (np.float32, "bilinear", 2, True),
+    (np.float64, "triangular", 1, True), (np.uint8, "nearest", 3, False),
+    (np.int16, "bilinear", 1, False), (np.float32, "triangular", 2, False)])
+def test_fused_resolve_sampling_equals_k5_then_k6(dtype, interp, n, keep_ij):
+    """xrs_rectify_ij_var (K6 sampled inside K5's resolve pass) == K5 then K6
+    bit for bit, and the ij image it keeps == K5's; device and host tiles,
+    a swath with NaN coordinates and degenerate quads."""
+    import torch
+
+    import xcube_resampling_amd as xrs
+    from xcube_resampling_amd import kernels
+    from xcube_resampling_amd import rectify as R
+
+    rng = np.random.default_rng(17)
+    h, w = 110, 95
+    jj, ii = np.mgrid[0:h, 0:w].astype(np.float64)
+    lon = 3.0 + 0.01 * ii + 0.002 * jj + rng.normal(0, 0.002, (h, w))
+    lat = 40.0 - 0.008 * jj + 0.001 * ii + rng.normal(0, 0.002, (h, w))
+    lat[40:42, 20] = np.nan
+    lon[60, 5] = lon[60, 4]
+    sgm = xrs.GridMapping.from_coords(xrs.DataArray(lon, ("y", "x"), name="lon"),
+                                      xrs.DataArray(lat, ("y", "x"), name="lat"), "EPSG:4326")
+    res = 0.006
+    x0 = float(np.floor(np.nanmin(lon) / res) * res)
+    y0 = float(np.floor(np.nanmin(lat) / res) * res)
+    size = (int(np.ceil((np.nanmax(lon) - x0) / res)), int(np.ceil((np.nanmax(lat) - y0) / res)))
+    tgm = xrs.GridMapping.regular(size, (x0, y0), res, "EPSG:4326", tile_size=(40, 36))
+    xy = (torch.from_numpy(lon).cuda(), torch.from_numpy(lat).cuda())
+    if np.issubdtype(dtype, np.integer):
+        var = rng.integers(0, 200, (n, h, w)).astype(dtype)
+        fill = 0
+    else:
+        var = rng.random((n, h, w)).astype(dtype)
+        fill = float("nan")
+    src = torch.from_numpy(var).cuda()
+    tiles, ntx, _, _ = R.rectify_tiles(sgm, tgm, xy=xy)
+    for t in (tiles, R._device_tiles(sgm, tgm, xy)):
+        ij = kernels.rectify_ij(xy[0], xy[1], t, ntx, tgm.height, tgm.width, tgm.x_res,
+                                -tgm.y_res, 1e-3)
+        exp = kernels.rectify_var(ij, src, interp, fill).cpu().numpy()
+        ij2, got = kernels.rectify_ij_var(xy[0], xy[1], t, tgm.height, tgm.width, tgm.x_res,
+                                          -tgm.y_res, 1e-3, src, interp, fill, keep_ij=keep_ij)
+        assert_bitwise_equal(got.cpu().numpy(), exp, f"fused {interp}")
+        if keep_ij:
+            assert_bitwise_equal(ij2.cpu().numpy(), ij.cpu().numpy(), "fused ij")
+        else:
+            assert ij2 is None
+    assert np.isfinite(ij.cpu().numpy()).sum() > 0.4 * ij[0].numel() * 2
+
+
+def test_rectify_dataset_fused_first_variable():
+    """rectify_dataset samples its first device variable inside K5: one and
+    two variables give the same values as each variable rectified alone."""
+    import xcube_resampling_amd as xrs
+
+    rng = np.random.default_rng(3)
+    h, w = 70, 64
+    jj, ii = np.mgrid[0:h, 0:w].astype(np.float64)
+    lon = 10.0 + 0.02 * ii + 0.004 * jj + rng.normal(0, 0.001, (h, w))
+    lat = 50.0 - 0.015 * jj + 0.003 * ii + rng.normal(0, 0.001, (h, w))
+    a = rng.random((h, w)).astype(np.float32)
+    b = rng.random((2, h, w))
+    coords = {"lon": xrs.DataArray(lon, ("y", "x")), "lat": xrs.DataArray(lat, ("y", "x"))}
+    both = xrs.Dataset(data_vars={"a": xrs.DataArray(a, ("y", "x")),
+                                  "b": xrs.DataArray(b, ("t", "y", "x"))}, coords=coords)
+    only_a = xrs.Dataset(data_vars={"a": xrs.DataArray(a, ("y", "x"))}, coords=coords)
+    only_b = xrs.Dataset(data_vars={"b": xrs.DataArray(b, ("t", "y", "x"))}, coords=coords)
+    kw = dict(interp_methods="bilinear", tile_size=32)
+    r2 = xrs.rectify_dataset(both, **kw)
+    ra = xrs.rectify_dataset(only_a, **kw)
+    rb = xrs.rectify_dataset(only_b, **kw)
+    assert_bitwise_equal(np.asarray(r2["a"].values), np.asarray(ra["a"].values), "a")
+    assert_bitwise_equal(np.asarray(r2["b"].values), np.asarray(rb["b"].values), "b")
+    assert isinstance(r2["a"].values, np.ndarray) and r2["b"].dims[0] == "t"
+    assert np.isfinite(r2["a"].values).mean() > 0.5
+
+
 def test_claim_fast_decisions_equal_exact_divisions():
     """K5a decides pixel windows and triangle hits by reciprocal
     multiplication with an exact-division fallback near every boundary; forcing

@@ -117,3 +117,111 @@ def test_gloo_band_sharded_hip_reprojection(tmp_path, case, balance):
             np.nan)
     assert got.dtype == exp.dtype == np.float64
     assert_bitwise_equal(got, exp, f"{case}/{balance}")   # NaN == NaN, -0 != +0
+
+
+# ---- coarsen and rectify splits on the HIP kernels ---------------------------------
+def _rank_coarsen_hip(rank, world, port, result_dir):
+    import sys
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    for p in (here, os.path.dirname(here)):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import torch
+    import torch.distributed as dist
+
+    from test_sharding_cpu import _coarsen_plan
+    from xcube_resampling_amd import kernels
+    from xcube_resampling_amd.sharding import coarsen_shard, gather_rows
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        plan, _ = _coarsen_plan()
+        a = np.random.default_rng(11).random((1, 160, 176)).astype(np.float32)
+        a.ravel()[::97] = np.nan
+        shard = coarsen_shard(plan, world, rank)
+        band = torch.from_numpy(np.ascontiguousarray(a[:, shard.src_row0:shard.src_row1])).cuda()
+        out = kernels.affine(band, shard.plan)   # the rank's source rows only
+        torch.cuda.synchronize()
+        whole = gather_rows(out.cpu(), plan.out_h)
+        if rank == 0:
+            np.save(os.path.join(result_dir, "coarsen.npy"), whole.numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_coarsen_shards_on_hip(tmp_path):
+    """Each of 2 ranks runs K3 (xrs_affine) on only the source rows of its
+    output chunk rows, with its re-based plan; the gathered result equals the
+    whole-array oracle bit for bit (affine.py:277-313)."""
+    import torch.multiprocessing as mp
+
+    from oracle import affine_ref
+    from test_sharding_cpu import _coarsen_plan
+
+    mp.spawn(_rank_coarsen_hip, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    _, m = _coarsen_plan()
+    a = np.random.default_rng(11).random((1, 160, 176)).astype(np.float32)
+    a.ravel()[::97] = np.nan
+    exp = np.asarray(affine_ref.resample_array(a, m, (1, 40, 44), (1, 8, 44), 1, "mean", False,
+                                               np.nan))
+    assert_bitwise_equal(np.load(tmp_path / "coarsen.npy"), exp, "coarsen on 2 ranks")
+
+
+def _rank_rectify_hip(rank, world, port, result_dir):
+    import sys
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    for p in (here, os.path.dirname(here)):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import torch
+    import torch.distributed as dist
+
+    import xcube_resampling_amd as xrs
+    from test_sharding_cpu import _rect_case
+    from xcube_resampling_amd import rectify as R
+    from xcube_resampling_amd.sharding import merge_tile_runs, rectify_shard
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        c = _rect_case()
+        sgm = xrs.GridMapping.from_coords(xrs.DataArray(c["lon"], ("y", "x"), name="lon"),
+                                          xrs.DataArray(c["lat"], ("y", "x"), name="lat"),
+                                          "EPSG:4326")
+        tgm = c["tgm"]
+        tiles, _, _, _ = R.rectify_tiles(sgm, tgm)
+        shard = rectify_shard(tiles, world, rank)
+        band = R.rectify_tile_run(sgm, tgm, torch.from_numpy(c["var"]).cuda(), shard,
+                                  "bilinear", np.nan, tiles=tiles)
+        parts = [None] * world
+        dist.all_gather_object(parts, (shard, band.cpu().numpy()))
+        if rank == 0:
+            w, h = c["size"]
+            np.save(os.path.join(result_dir, "rectify.npy"),
+                    merge_tile_runs(parts, tiles, (h, w), np.nan))
+            np.save(os.path.join(result_dir, "tiles.npy"), tiles.view(np.uint8))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_rectify_tile_shards_on_hip(tmp_path):
+    """Each of 2 ranks runs K5 on its cost-balanced run of target tiles and K6
+    on the rows they cover; the merged raster equals the oracle bit for bit
+    (rectify.py:347-370, 605-734)."""
+    import torch.multiprocessing as mp
+
+    from oracle import rectify_ref
+    from test_sharding_cpu import _rect_case
+
+    mp.spawn(_rank_rectify_hip, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    c = _rect_case()
+    got_tiles = np.load(tmp_path / "tiles.npy").view(c["tiles"].dtype)
+    assert np.array_equal(got_tiles.view(np.uint8), c["tiles"].view(np.uint8))   # same tiling
+    exp = rectify_ref.compute_var_image(c["ij"], c["var"], np.nan, "bilinear", c["tile"])
+    assert np.isfinite(exp).mean() > 0.5
+    assert_bitwise_equal(np.load(tmp_path / "rectify.npy"), exp, "rectify on 2 ranks")

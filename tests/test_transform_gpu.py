@@ -172,6 +172,35 @@ def test_fused_projection_gather_equals_tables_path(src_crs, dst_crs, dtype, int
     assert str(src.device) not in fused._device_cache   # no coordinate tables were made
 
 
+def test_empty_band_raises_on_both_paths():
+    """A zero-row source band (sharding hands a rank no source rows) at a
+    row its target rows do read: the table path and the fused-projection
+    path both report the out-of-band read (XRS_EFLAG_BAND) — neither reads
+    the one-row placeholder as data."""
+    import dataclasses
+
+    import torch
+
+    import xcube_resampling_amd as xrs
+    from xcube_resampling_amd import _native, kernels
+
+    sgm = xrs.GridMapping.regular((900, 700), (400000.0, 5500000.0), 100.0, "EPSG:32632",
+                                  tile_size=256)
+    tgm = xrs.GridMapping.regular((800, 640), (4100000.0, 2900000.0), 110.0, "EPSG:3035",
+                                  tile_size=(256, 192))
+    plan = xrs.plan_reproject(sgm, tgm, xrs.Transformer.from_crs(tgm.crs, sgm.crs,
+                                                                  always_xy=True))
+    fused = dataclasses.replace(plan, fuse_transform=True, _device_cache={})
+    rows = (40, 100)
+    j0, j1 = plan.source_rows_for(*rows)
+    assert j1 > j0
+    band = torch.zeros((1, 0, 900), dtype=torch.float32, device="cuda")
+    for p in (plan, fused):
+        with pytest.raises(_native.NativeLibraryError, match="source band"):
+            kernels.reproject(band, p, "nearest", 0.0, rows=rows, src_row0=j0)
+    assert str(band.device) not in fused._device_cache
+
+
 def test_streamed_host_source_fuses_when_tables_exceed_budget():
     """A host-resident source (band pipeline of streaming.reproject_host) on a
     non-separable pair with the table budget at 0: the projection runs inside

@@ -54,17 +54,13 @@ __device__ inline void clenS(const double* a, double sin_arg_r, double cos_arg_r
   di = r * hi + i * hr;
 }
 
-__device__ inline void tmerc_fwd(const XrsProjStep& s, double lam, double phi, double& x,
-                                 double& y) {
-  const double* cbg = s.c + 6;
+// tmerc_fwd from the sines and cosines of the Gaussian latitude Cn and the
+// longitude (shared by tmerc_fwd and the LAEA -> tmerc pipeline below)
+__device__ inline void tmerc_fwd_tail(const XrsProjStep& s, double sin_Cn, double cos_Cn,
+                                      double sin_Ce, double cos_Ce, double& x, double& y) {
   const double* gtu = s.c + 18;
-  double s2p, c2p, sin_Cn, cos_Cn, sin_Ce, cos_Ce;
-  sincos(2 * phi, &s2p, &c2p);
-  double Cn = gatg(cbg, phi, c2p, s2p);
-  sincos(Cn, &sin_Cn, &cos_Cn);
-  sincos(lam, &sin_Ce, &cos_Ce);
   const double cos_Cn_cos_Ce = cos_Cn * cos_Ce;
-  Cn = atan2(sin_Cn, cos_Cn_cos_Ce);
+  double Cn = atan2(sin_Cn, cos_Cn_cos_Ce);
   const double inv_denom_tan_Ce = 1.0 / hypot(sin_Cn, cos_Cn_cos_Ce);
   const double tan_Ce = sin_Ce * cos_Cn * inv_denom_tan_Ce;
   double Ce = asinh(tan_Ce);
@@ -82,6 +78,17 @@ __device__ inline void tmerc_fwd(const XrsProjStep& s, double lam, double phi, d
   const bool ok = fabs(Ce) <= 2.623395162778;
   x = ok ? s.Qn * Ce : INFINITY;
   y = ok ? s.Qn * Cn + s.Zb : INFINITY;
+}
+
+__device__ inline void tmerc_fwd(const XrsProjStep& s, double lam, double phi, double& x,
+                                 double& y) {
+  const double* cbg = s.c + 6;
+  double s2p, c2p, sin_Cn, cos_Cn, sin_Ce, cos_Ce;
+  sincos(2 * phi, &s2p, &c2p);
+  const double Cn = gatg(cbg, phi, c2p, s2p);
+  sincos(Cn, &sin_Cn, &cos_Cn);
+  sincos(lam, &sin_Ce, &cos_Ce);
+  tmerc_fwd_tail(s, sin_Cn, cos_Cn, sin_Ce, cos_Ce, x, y);
 }
 
 __device__ inline void tmerc_inv(const XrsProjStep& s, double x, double y, double& lam,
@@ -207,6 +214,94 @@ __device__ inline double adjlon(double lam) {
   return w;
 }
 
+// ---- LAEA inverse -> tmerc forward through sines and cosines --------------------
+// The pipeline of a LAEA target grid over a UTM source (config 2u: EPSG:3035 ->
+// EPSG:32632, reproject.py:472-496 per target pixel).  Every intermediate
+// angle of apply_step<LAEA_INV> + apply_step<TMERC_FWD> is consumed only
+// through its sine and cosine until tmerc's final atan2 / asinh, so they are
+// carried as (sin, cos) pairs: 2 asin(a) by the double-angle identities,
+// atan2(X, Y) as (X, Y) / hypot(X, Y), the longitude shift lam0_laea -
+// lam0_tmerc and the latitude corrections of authlat (|d| < 0.003) and gatg
+// (|d| < 0.004) as rotations (the small angles by Taylor terms to below an ulp).
+// Ten f64 transcendentals per point (asin x2, sincos x5, atan2, ...) become
+// two square roots, two hypots and two divisions; results agree with the
+// two-step restatement to a few ulps (tests/test_transform_gpu.py tolerances),
+// non-finite in the same places (the same `bad` / `ok` decisions).
+struct LaeaTmerc {
+  double sd, cd;     // sin / cos (lam0_laea - lam0_tmerc)
+  double sp0, cp0;   // sin / cos phi0 (the LAEA centre, where rho < 1e-10)
+};
+
+__device__ inline LaeaTmerc laea_tmerc_setup(const XrsProjStep& s0, const XrsProjStep& s1) {
+  LaeaTmerc k;
+  sincos(s0.lam0 - s1.lam0, &k.sd, &k.cd);
+  sincos(s0.phi0, &k.sp0, &k.cp0);
+  return k;
+}
+
+// sin / cos of a small angle (|d| < 0.01): the dropped terms are < 1e-18
+__device__ inline void sincos_small(double d, double& s, double& c) {
+  const double d2 = d * d;
+  s = d - d * d2 * (1.0 / 6.0) * (1.0 - d2 * (1.0 / 20.0));
+  c = 1.0 - 0.5 * d2 * (1.0 - d2 * (1.0 / 12.0));
+}
+
+template <bool OBLIQ>
+__device__ inline void laea_inv_tmerc_fwd(const XrsProjStep& s0, const XrsProjStep& s1,
+                                          const LaeaTmerc& k, double& x, double& y) {
+  // laea_inv's first half, operation for operation (the `small` / `bad`
+  // decisions must be the two-step pipeline's)
+  double xx = (x - s0.x0) * s0.ra, yy = (y - s0.y0) * s0.ra;
+  xx = xx / s0.dd;
+  yy = yy * s0.dd;
+  const double rho = hypot(xx, yy);
+  const bool small = rho < kEps10;
+  const double rho_s = small ? 1.0 : rho;
+  const double a = 0.5 * rho_s / s0.rq;
+  const bool bad = a > 1.0;
+  const double ac = bad ? 1.0 : a;   // NaN stays NaN
+  const double ca = sqrt((1.0 - ac) * (1.0 + ac));
+  const double sCe = 2.0 * ac * ca;             // sin (2 asin ac)
+  const double cCe = 1.0 - 2.0 * ac * ac;       // cos (2 asin ac)
+  const double X = xx * sCe;
+  double ab, Y;
+  if constexpr (OBLIQ) {
+    ab = cCe * s0.sinb1 + yy * sCe * s0.cosb1 / rho_s;
+    Y = rho_s * s0.cosb1 * cCe - yy * s0.sinb1 * sCe;
+  } else {
+    ab = yy * sCe / rho_s;
+    Y = rho_s * cCe;
+  }
+  // longitude atan2(X, Y) (0 at the centre), shifted to tmerc's central meridian
+  const double r = hypot(X, Y);
+  const bool r0 = small || r == 0.0;
+  const double ir = 1.0 / (r0 ? 1.0 : r);
+  const double sl = r0 ? 0.0 : X * ir;
+  const double cl = r0 ? ((small || !signbit(Y)) ? 1.0 : -1.0) : Y * ir;
+  const double sin_Ce = sl * k.cd + cl * k.sd;
+  const double cos_Ce = cl * k.cd - sl * k.sd;
+  // latitude: beta = asin(clip(ab)), phi = authlat(beta) = beta + d
+  const double sb = clip1(ab);
+  const double cb = sqrt((1.0 - sb) * (1.0 + sb));
+  const double s2b = 2.0 * sb * cb, c2b = (cb - sb) * (cb + sb);
+  const double s4b = 2.0 * s2b * c2b, c4b = (c2b - s2b) * (c2b + s2b);
+  const double s6b = s4b * c2b + c4b * s2b;
+  double sd, cd;
+  sincos_small(s0.apa[0] * s2b + s0.apa[1] * s4b + s0.apa[2] * s6b, sd, cd);
+  const double sphi = small ? k.sp0 : sb * cd + cb * sd;
+  const double cphi = small ? k.cp0 : cb * cd - sb * sd;
+  // tmerc_fwd: Gaussian latitude Cn = phi + gatg correction
+  const double s2p = 2.0 * sphi * cphi, c2p = (cphi - sphi) * (cphi + sphi);
+  double sg, cg;
+  sincos_small(gatg(s1.c + 6, 0.0, c2p, s2p), sg, cg);
+  const double sin_Cn = sphi * cg + cphi * sg;
+  const double cos_Cn = cphi * cg - sphi * sg;
+  double px, py;
+  tmerc_fwd_tail(s1, sin_Cn, cos_Cn, sin_Ce, cos_Ce, px, py);
+  x = bad ? INFINITY : s1.a * px + s1.x0;
+  y = bad ? INFINITY : s1.a * py + s1.y0;
+}
+
 // one pipeline step (crs._projection forward / inverse, webmerc_forward /
 // _inverse); the kind is a template parameter, so a kernel holds only the code
 // (and registers) of its own pipeline
@@ -240,6 +335,33 @@ __device__ inline void apply_step(const XrsProjStep& s, double& x, double& y) {
     y = phi * rad_to_deg;
   }
 }
+
+// pipeline = step K0 then step K1 (0: none); FAST 1 / 2: the LAEA (oblique /
+// equatorial) -> tmerc pair through laea_inv_tmerc_fwd (chosen on the host,
+// fast_kind), with its per-thread constants set up once
+constexpr int kFastNone = 0, kFastObliq = 1, kFastEquit = 2;
+
+inline int fast_kind(int k0, int k1, const XrsProjStep& s0) {
+  if (k0 != XRS_PROJ_LAEA_INV || k1 != XRS_PROJ_TMERC_FWD) return kFastNone;
+  return s0.mode == kObliq ? kFastObliq : (s0.mode == kEquit ? kFastEquit : kFastNone);
+}
+
+template <int K0, int K1, int FAST>
+struct Pipeline {
+  LaeaTmerc k{};
+  __device__ Pipeline(const XrsProjStep& s0, const XrsProjStep& s1) {
+    if constexpr (FAST != kFastNone) k = laea_tmerc_setup(s0, s1);
+  }
+  __device__ void operator()(const XrsProjStep& s0, const XrsProjStep& s1, double& x,
+                             double& y) const {
+    if constexpr (FAST != kFastNone) {
+      laea_inv_tmerc_fwd<FAST == kFastObliq>(s0, s1, k, x, y);
+    } else {
+      if constexpr (K0 != 0) apply_step<K0>(s0, x, y);
+      if constexpr (K1 != 0) apply_step<K1>(s1, x, y);
+    }
+  }
+};
 
 }  // namespace proj
 }  // namespace xrs

@@ -418,7 +418,11 @@ constexpr double kMaxFormMargin = 1e-3;   // larger bound: exact test at every p
 // One triangle's three affine forms over the quad's pixel window (float32)
 // and the decision threshold thr = -2M.  form(a, b) = c0 + a ci + b cj.
 struct TriForms {
-  float c[9];   // (c0, ci, cj) of u - umin - M, v - umin - M, uvmax - M - (u + v)
+  // (c0, ci, cj) of u - umin - M, v - umin - M, uvmax - M - (u + v); named
+  // members, not an array: an array of these (read as overlapping float
+  // pairs by the packed walk) was kept in memory — the compiler put it in
+  // LDS, one 40-byte slot per lane, with bank conflicts on every read
+  float u0, ui, uj, v0, vi, vj, w0, wi, wj;
   float thr;
 };
 
@@ -440,10 +444,10 @@ struct TriForms {
 // up by 1.01 for its own rounding.  Returns false (every pixel of the window
 // to the exact test) when M is NaN / inf or above kMaxFormMargin (degenerate
 // triangles).
-__device__ inline bool tri_setup(double ex64, double ey64, double e1_64, double e2_64,
-                                 double e3_64, double e4_64, double det, float sx, float sy,
-                                 float X, float Y, float ax, float ay, float wn, float hn,
-                                 float umin, float uvmax, float margin_scale, TriForms& F) {
+__device__ inline TriForms tri_setup(double ex64, double ey64, double e1_64, double e2_64,
+                                     double e3_64, double e4_64, double det, float sx, float sy,
+                                     float X, float Y, float ax, float ay, float wn, float hn,
+                                     float umin, float uvmax, float margin_scale, bool& ok) {
   const float ex = (float)ex64, ey = (float)ey64;
   const float e1 = (float)e1_64, e2 = (float)e2_64, e3 = (float)e3_64, e4 = (float)e4_64;
   const float r = __builtin_amdgcn_rcpf((float)det), ar = fabsf(r);
@@ -457,12 +461,9 @@ __device__ inline bool tri_setup(double ex64, double ey64, double e1_64, double 
   const float R = ((X + ax) * (fabsf(e1) + fabsf(e4)) + (Y + ay) * (fabsf(e2) + fabsf(e3))) * ar;
   const float M = 2.02f * ((float)kEps32 * E + 10.0f * (float)kEps64 * R +
                            8.0f * (float)kEps64 * T) * margin_scale;
-  if (!(M <= (float)kMaxFormMargin * margin_scale)) return false;
-  F.c[0] = (u0 - umin) - M; F.c[1] = ui; F.c[2] = uj;
-  F.c[3] = (v0 - umin) - M; F.c[4] = vi; F.c[5] = vj;
-  F.c[6] = (uvmax - (u0 + v0)) - M; F.c[7] = -(ui + vi); F.c[8] = -(uj + vj);
-  F.thr = -2.0f * M;
-  return true;
+  ok = M <= (float)kMaxFormMargin * margin_scale;
+  return TriForms{(u0 - umin) - M, ui, uj, (v0 - umin) - M, vi, vj,
+                  (uvmax - (u0 + v0)) - M, -(ui + vi), -(uj + vj), -2.0f * M};
 }
 
 // the reference's test of one triangle at pixel centre (dx, dy)
@@ -487,27 +488,29 @@ __device__ inline bool tri_exact(const Quad& q, bool tri_b, double dx, double dy
 // One triangle's forms for the pair walk: 1 = forms set up, 0 = no triangle
 // (_fdet NaN or 0: never hits; forms that are -inf everywhere), -1 = no usable
 // bound (the lane takes the reference's test over the untrimmed window).
-__device__ inline int tri_forms(double ex, double ey, double e1, double e2, double e3,
-                                double e4, double cx, double cy, const RectArgs& a, float X,
-                                float Y, float wn, float hn, float umin, float uvmax,
-                                TriForms& F) {
+// (returned by value, status in `st`: the forms stay in registers)
+__device__ inline TriForms tri_forms(double ex, double ey, double e1, double e2, double e3,
+                                     double e4, double cx, double cy, const RectArgs& a,
+                                     float X, float Y, float wn, float hn, float umin,
+                                     float uvmax, int& st) {
   const double det = e3 * e1 - e2 * e4;   // _fdet from the edge factors
   if (det != det || det == 0.0) {
-#pragma unroll
-    for (int i = 0; i < 9; ++i) F.c[i] = 0.0f;
-    F.c[0] = -INFINITY;
-    F.thr = 0.0f;
-    return 0;
+    st = 0;
+    return TriForms{-INFINITY, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
   }
-  return tri_setup(ex, ey, e1, e2, e3, e4, det, (float)a.x_scale, (float)a.y_scale, X, Y,
-                   fabsf((float)cx), fabsf((float)cy), wn, hn, umin, uvmax, a.margin_scale, F)
-             ? 1 : -1;
+  bool ok;
+  const TriForms F = tri_setup(ex, ey, e1, e2, e3, e4, det, (float)a.x_scale, (float)a.y_scale,
+                               X, Y, fabsf((float)cx), fabsf((float)cy), wn, hn, umin, uvmax,
+                               a.margin_scale, ok);
+  st = ok ? 1 : -1;
+  return F;
 }
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
-__device__ inline f32x2 form2(const TriForms& A, const TriForms& B, int i, f32x2 av, f32x2 bv) {
-  const f32x2 c0 = {A.c[i], B.c[i]}, ci = {A.c[i + 1], B.c[i + 1]}, cj = {A.c[i + 2], B.c[i + 2]};
+__device__ inline f32x2 form2(float a0, float ai, float aj, float b0, float bi, float bj,
+                              f32x2 av, f32x2 bv) {
+  const f32x2 c0 = {a0, b0}, ci = {ai, bi}, cj = {aj, bj};
   return __builtin_elementwise_fma(bv, cj, __builtin_elementwise_fma(av, ci, c0));
 }
 
@@ -515,13 +518,15 @@ __device__ inline f32x2 form2(const TriForms& A, const TriForms& B, int i, f32x2
 // once: triangle A in the low and B in the high half of packed float32 FMAs
 // (v_pk_fma_f32).  Returns (hit, undecided) bit masks: hit when some
 // triangle's min3 >= 0, undecided when neither hits and some min3 >= -2M.
-__device__ inline uint2 walk_pair(const TriForms& A, const TriForms& B, int n, int nw) {
+__device__ inline uint2 walk_pair(const TriForms A, const TriForms B, int n, int nw) {
   uint32_t h_hit = 0, h_uns = 0;
   float af = 0.0f, bf = 0.0f;
   int col = 0;
   for (int k = 0; k < n; ++k) {
     const f32x2 av = {af, af}, bv = {bf, bf};
-    const f32x2 u = form2(A, B, 0, av, bv), v = form2(A, B, 3, av, bv), w = form2(A, B, 6, av, bv);
+    const f32x2 u = form2(A.u0, A.ui, A.uj, B.u0, B.ui, B.uj, av, bv);
+    const f32x2 v = form2(A.v0, A.vi, A.vj, B.v0, B.vi, B.vj, av, bv);
+    const f32x2 w = form2(A.w0, A.wi, A.wj, B.w0, B.wi, B.wj, av, bv);
     const float ha = fminf(u.x, fminf(v.x, w.x)), hb = fminf(u.y, fminf(v.y, w.y));
     const uint32_t bit = 1u << k;
     h_hit |= fmaxf(ha, hb) >= 0.0f ? bit : 0u;
@@ -632,26 +637,37 @@ __device__ inline void claim_exact_lane(const RectArgs& a, const TileInfo& ti, i
   }
 }
 
+template <bool LDS_OFFS>   // offsets staged in LDS (up to kClaimOffsLds tiles) or read from HBM
 __global__ void __launch_bounds__(kClaimThreads)
 rectify_claim_kernel(RectArgs a) {
   __shared__ int64_t offs_s[kClaimOffsLds + 1];
   const int lane = threadIdx.x & 63;
-  const bool lds_offs = a.ntiles <= kClaimOffsLds;
+  constexpr bool lds_offs = LDS_OFFS;
   if (lds_offs)
     for (int64_t t = threadIdx.x; t <= a.ntiles; t += kClaimThreads) offs_s[t] = a.chunk_offs[t];
   __syncthreads();
-  const int64_t* offs = lds_offs ? offs_s : a.chunk_offs;
-  const int64_t nchunks = offs[a.ntiles];
+  // the offsets are read from the LDS copy or from global memory in two
+  // instantiations: one pointer to either is a generic (flat) pointer, whose
+  // loads wait on both the LDS and the vector-memory counters
+  const int64_t nchunks = lds_offs ? offs_s[a.ntiles] : a.chunk_offs[a.ntiles];
   const double umin = -a.uv_delta, uvmax = 1.0 + 2 * a.uv_delta;
   const int64_t nwaves = (int64_t)gridDim.x * (kClaimThreads / 64);
   for (int64_t c = (int64_t)blockIdx.x * (kClaimThreads / 64) + (threadIdx.x >> 6); c < nchunks;
        c += nwaves) {
-    int64_t lo = 0, hi = a.ntiles;   // last t with offs[t] <= c
-    while (hi - lo > 1) {
-      const int64_t m = (lo + hi) >> 1;
-      if (offs[m] <= c) lo = m; else hi = m;
+    int64_t lo = 0, hi = a.ntiles;   // last t with offs[t] <= c (c is wave-uniform)
+    if (lds_offs) {
+      while (hi - lo > 1) {
+        const int64_t m = (lo + hi) >> 1;
+        if (offs_s[m] <= c) lo = m; else hi = m;
+      }
+    } else {
+      while (hi - lo > 1) {
+        const int64_t m = (lo + hi) >> 1;
+        if (a.chunk_offs[m] <= c) lo = m; else hi = m;
+      }
     }
     lo = __builtin_amdgcn_readfirstlane((int32_t)lo);   // wave-uniform
+    const int64_t off_lo = lds_offs ? offs_s[lo] : a.chunk_offs[lo];
     const TileInfo ti = a.tiles[lo];
     if (!tile_ok(a, ti) || ti.si0 < 0) {   // wave-uniform
       if (lane == 0) atomicOr(a.err_flags, XRS_EFLAG_STATE);
@@ -659,7 +675,7 @@ rectify_claim_kernel(RectArgs a) {
     }
     const int32_t nq_i = ti.swin - 1, nq_j = ti.shin - 1;
     const int32_t ncx = (nq_i + kStripW - 1) / kStripW;
-    const int32_t cc = (int32_t)(c - offs[lo]);
+    const int32_t cc = (int32_t)(c - off_lo);
     const int32_t cy = cc / ncx, cx = cc - cy * ncx;
     const int32_t pcol = cx * kStripW + lane;          // point column in the window
     const bool has_pt = pcol <= nq_i;
@@ -736,13 +752,13 @@ rectify_claim_kernel(RectArgs a) {
               const float wn = (float)(nw - 1), hn = (float)(nh - 1);
               // A = (p0, p1, p2): _fu(p, p0, p2), _fv(p, p0, p1), _fdet(p0, p1, p2)
               // B = (p3, p2, p1): _fu(p, p3, p1), _fv(p, p3, p2), _fdet(p3, p2, p1)
-              TriForms FA, FB;
-              const int sa = tri_forms(t0.x - dx0, t0.y - dy0, t0.y - b0.y, t0.x - b0.x,
-                                       t0.x - t1.x, t0.y - t1.y, t0.x, t0.y, a, X, Y, wn, hn,
-                                       (float)umin, (float)uvmax, FA);
-              const int sb = tri_forms(b1.x - dx0, b1.y - dy0, b1.y - t1.y, b1.x - t1.x,
-                                       b1.x - b0.x, b1.y - b0.y, b1.x, b1.y, a, X, Y, wn, hn,
-                                       (float)umin, (float)uvmax, FB);
+              int sa, sb;
+              const TriForms FA = tri_forms(t0.x - dx0, t0.y - dy0, t0.y - b0.y, t0.x - b0.x,
+                                            t0.x - t1.x, t0.y - t1.y, t0.x, t0.y, a, X, Y, wn,
+                                            hn, (float)umin, (float)uvmax, sa);
+              const TriForms FB = tri_forms(b1.x - dx0, b1.y - dy0, b1.y - t1.y, b1.x - t1.x,
+                                            b1.x - b0.x, b1.y - b0.y, b1.x, b1.y, a, X, Y, wn,
+                                            hn, (float)umin, (float)uvmax, sb);
               if (sa < 0 || sb < 0) {
                 slow = true;   // a triangle without a usable bound: exact, untrimmed window
               } else if (sa | sb) {
@@ -832,6 +848,73 @@ rectify_claim_kernel(RectArgs a) {
   }
 }
 
+// ---- K6: per-variable sampling (rectify.py:663-734) ------------------------------
+// One target pixel p of every dim-0 slice at source position (fi, fj); NaN
+// positions -> fill.  Positions outside the source (never made by K5:
+// src_i_min + src_i <= w - 1, rectify.py:574-576) are filled and reported
+// (`bad`), never dereferenced.
+template <typename T, int INTERP>
+__device__ inline void sample_px(double fi, double fj, const T* __restrict__ src, int64_t n,
+                                 int64_t src_h, int64_t src_w, int64_t src_sn, int64_t src_sy,
+                                 T* __restrict__ dst, int64_t dst_sn, int64_t p, T tfill,
+                                 bool& bad) {
+  if (fi != fi || fj != fj) {
+    for (int64_t s = 0; s < n; ++s) dst[s * dst_sn + p] = tfill;
+    return;
+  }
+  if (!(fi >= 0.0 && fi < (double)src_w && fj >= 0.0 && fj < (double)src_h)) {
+    bad = true;
+    for (int64_t s = 0; s < n; ++s) dst[s * dst_sn + p] = tfill;
+    return;
+  }
+  int64_t i0 = (int64_t)fi, j0 = (int64_t)fj;   // int() truncation (values >= 0)
+  const double u = fi - (double)i0, v = fj - (double)j0;
+  const int64_t imax = src_w - 1, jmax = src_h - 1;
+  if (INTERP == XRS_INTERP_NEAREST) {
+    if (u > 0.5) i0 = min(max(i0 + 1, (int64_t)0), imax);
+    if (v > 0.5) j0 = min(max(j0 + 1, (int64_t)0), jmax);
+    for (int64_t s = 0; s < n; ++s) dst[s * dst_sn + p] = src[s * src_sn + j0 * src_sy + i0];
+    return;
+  }
+  const int64_t i1 = min(max(i0 + 1, (int64_t)0), imax), j1 = min(max(j0 + 1, (int64_t)0), jmax);
+  for (int64_t s = 0; s < n; ++s) {
+    const T* S = src + s * src_sn;
+    double val;
+    const double v01 = (double)S[j0 * src_sy + i1], v10 = (double)S[j1 * src_sy + i0];
+    if (INTERP == XRS_INTERP_TRIANGULAR) {
+      if (u + v < 1.0) {
+        const double v00 = (double)S[j0 * src_sy + i0];
+        val = v00 + u * (v01 - v00) + v * (v10 - v00);
+      } else {
+        const double v11 = (double)S[j1 * src_sy + i1];
+        val = v11 + (1.0 - u) * (v10 - v11) + (1.0 - v) * (v01 - v11);
+      }
+    } else {
+      const double v00 = (double)S[j0 * src_sy + i0], v11 = (double)S[j1 * src_sy + i1];
+      const double u0 = v00 + u * (v01 - v00);
+      const double u1 = v10 + u * (v11 - v10);
+      val = u0 + v * (u1 - u0);
+    }
+    dst[s * dst_sn + p] = Conv<T>::from_f64(val);
+  }
+}
+
+template <typename T, int INTERP>
+__global__ void __launch_bounds__(kThreads)
+rectify_var_kernel(const double* __restrict__ ij, int64_t ij_sn, int64_t dst_h, int64_t dst_w,
+                   const T* __restrict__ src, int64_t n, int64_t src_h, int64_t src_w,
+                   int64_t src_sn, int64_t src_sy, T* __restrict__ dst, int64_t dst_sn,
+                   double fill, int32_t* err_flags) {
+  const int64_t np = dst_h * dst_w;
+  const T tfill = Conv<T>::from_f64(fill);
+  bool bad = false;
+  for (int64_t p = (int64_t)blockIdx.x * kThreads + threadIdx.x; p < np;
+       p += (int64_t)gridDim.x * kThreads)
+    sample_px<T, INTERP>(ij[p], ij[ij_sn + p], src, n, src_h, src_w, src_sn, src_sy, dst,
+                         dst_sn, p, tfill, bad);
+  if (bad) atomicOr(err_flags, XRS_EFLAG_STATE);
+}
+
 // ---- K5b: resolve the winning quad of every target pixel ------------------------
 // Work item = one tile x kResolveRows target rows (tile fields are block-
 // uniform: no per-pixel tile search or 64-bit division); each thread takes one
@@ -840,19 +923,34 @@ rectify_claim_kernel(RectArgs a) {
 // dependent memory round trips per kResolveRows pixels instead of per pixel.
 constexpr int kResolveRows = 4;
 
+// A variable sampled by the resolve pass itself (K6 fused into K5b: the
+// first variable of a rectification needs no ij image round trip through HBM).
+struct FusedVar {
+  const void* src;
+  int64_t n, src_h, src_w, src_sn, src_sy;
+  void* dst;
+  int64_t dst_sn;
+  double fill;
+  int interp;      // XRS_INTERP_*
+  int write_ij;    // 0: the ij image is not needed by any other variable
+};
+
+template <typename T, bool FUSE>
 __global__ void __launch_bounds__(kThreads)
-rectify_resolve_kernel(RectArgs a) {
+rectify_resolve_kernel(RectArgs a, FusedVar fv) {
   const int64_t n = a.dst_h * a.dst_w;
+  const T tfill = FUSE ? Conv<T>::from_f64(fv.fill) : T{};
   // tile 0 has the full tile height (edge tiles are shorter)
   const int64_t bands = (a.tiles[0].th + kResolveRows - 1) / kResolveRows;
   const int64_t nitems = a.ntiles * bands;
   const double inv_w = 1.0 / (double)a.w;
+  bool bad = false;
   for (int64_t it = blockIdx.x; it < nitems; it += gridDim.x) {
     const int64_t t = it / bands;
     const int32_t rb = (int32_t)(it - t * bands) * kResolveRows;
     const TileInfo ti = a.tiles[t];
     if (!tile_ok(a, ti)) {   // block-uniform
-      if (threadIdx.x == 0) atomicOr(a.err_flags, XRS_EFLAG_STATE);
+      bad = true;
       continue;
     }
     if (rb >= ti.th) continue;
@@ -872,14 +970,15 @@ rectify_resolve_kernel(RectArgs a) {
           int64_t j = (int64_t)((double)key[r] * inv_w);
           int64_t i = (int64_t)key[r] - j * a.w;
           if (i < 0) { --j; i += a.w; } else if (i >= a.w) { ++j; i -= a.w; }
-          if (j < 0 || j > a.h - 2 || i < 0 || i > a.w - 2) {   // not a quad's key
-            atomicOr(a.err_flags, XRS_EFLAG_STATE);
-            key[r] = 0xFFFFFFFFu;
-            continue;
-          }
-          qj[r] = j;
-          qi[r] = i;
-          Q[r] = load_quad(a, j, i);
+          // a key that is no quad's (inconsistent inputs) is reported and
+          // dropped; selects, not a branch: the corner loads of all rows stay
+          // in flight together
+          const bool ok = j >= 0 && j <= a.h - 2 && i >= 0 && i <= a.w - 2;
+          bad |= !ok;
+          key[r] = ok ? key[r] : 0xFFFFFFFFu;
+          qj[r] = ok ? j : 0;
+          qi[r] = ok ? i : 0;
+          Q[r] = load_quad(a, qj[r], qi[r]);
         }
       }
 #pragma unroll
@@ -909,70 +1008,30 @@ rectify_resolve_kernel(RectArgs a) {
           }
         }
         const int64_t p = p0 + r * a.dst_w;
-        a.ij[p] = oi;
-        a.ij[n + p] = oj;
+        if (!FUSE || fv.write_ij) {
+          a.ij[p] = oi;
+          a.ij[n + p] = oj;
+        }
+        if constexpr (FUSE) {
+          const T* src = static_cast<const T*>(fv.src);
+          T* dst = static_cast<T*>(fv.dst);
+          if (fv.interp == XRS_INTERP_NEAREST)
+            sample_px<T, XRS_INTERP_NEAREST>(oi, oj, src, fv.n, fv.src_h, fv.src_w, fv.src_sn,
+                                             fv.src_sy, dst, fv.dst_sn, p, tfill, bad);
+          else if (fv.interp == XRS_INTERP_TRIANGULAR)
+            sample_px<T, XRS_INTERP_TRIANGULAR>(oi, oj, src, fv.n, fv.src_h, fv.src_w,
+                                                fv.src_sn, fv.src_sy, dst, fv.dst_sn, p, tfill,
+                                                bad);
+          else
+            sample_px<T, XRS_INTERP_BILINEAR>(oi, oj, src, fv.n, fv.src_h, fv.src_w, fv.src_sn,
+                                              fv.src_sy, dst, fv.dst_sn, p, tfill, bad);
+        }
       }
     }
   }
+  if (bad) atomicOr(a.err_flags, XRS_EFLAG_STATE);
 }
 
-// ---- K6: per-variable sampling (rectify.py:663-734) ------------------------------
-template <typename T, int INTERP>
-__global__ void __launch_bounds__(kThreads)
-rectify_var_kernel(const double* __restrict__ ij, int64_t ij_sn, int64_t dst_h, int64_t dst_w,
-                   const T* __restrict__ src, int64_t n, int64_t src_h, int64_t src_w,
-                   int64_t src_sn, int64_t src_sy, T* __restrict__ dst, int64_t dst_sn,
-                   double fill, int32_t* err_flags) {
-  const int64_t np = dst_h * dst_w;
-  const T tfill = Conv<T>::from_f64(fill);
-  bool bad = false;
-  for (int64_t p = (int64_t)blockIdx.x * kThreads + threadIdx.x; p < np;
-       p += (int64_t)gridDim.x * kThreads) {
-    const double fi = ij[p], fj = ij[ij_sn + p];
-    if (fi != fi || fj != fj) {
-      for (int64_t s = 0; s < n; ++s) dst[s * dst_sn + p] = tfill;
-      continue;
-    }
-    // K5 positions lie inside the source (src_i_min + src_i <= w - 1,
-    // rectify.py:574-576); anything else is reported, never dereferenced
-    if (!(fi >= 0.0 && fi < (double)src_w && fj >= 0.0 && fj < (double)src_h)) {
-      bad = true;
-      for (int64_t s = 0; s < n; ++s) dst[s * dst_sn + p] = tfill;
-      continue;
-    }
-    int64_t i0 = (int64_t)fi, j0 = (int64_t)fj;   // int() truncation (values >= 0)
-    const double u = fi - (double)i0, v = fj - (double)j0;
-    const int64_t imax = src_w - 1, jmax = src_h - 1;
-    if (INTERP == XRS_INTERP_NEAREST) {
-      if (u > 0.5) i0 = min(max(i0 + 1, (int64_t)0), imax);
-      if (v > 0.5) j0 = min(max(j0 + 1, (int64_t)0), jmax);
-      for (int64_t s = 0; s < n; ++s) dst[s * dst_sn + p] = src[s * src_sn + j0 * src_sy + i0];
-      continue;
-    }
-    const int64_t i1 = min(max(i0 + 1, (int64_t)0), imax), j1 = min(max(j0 + 1, (int64_t)0), jmax);
-    for (int64_t s = 0; s < n; ++s) {
-      const T* S = src + s * src_sn;
-      double val;
-      const double v01 = (double)S[j0 * src_sy + i1], v10 = (double)S[j1 * src_sy + i0];
-      if (INTERP == XRS_INTERP_TRIANGULAR) {
-        if (u + v < 1.0) {
-          const double v00 = (double)S[j0 * src_sy + i0];
-          val = v00 + u * (v01 - v00) + v * (v10 - v00);
-        } else {
-          const double v11 = (double)S[j1 * src_sy + i1];
-          val = v11 + (1.0 - u) * (v10 - v11) + (1.0 - v) * (v01 - v11);
-        }
-      } else {
-        const double v00 = (double)S[j0 * src_sy + i0], v11 = (double)S[j1 * src_sy + i1];
-        const double u0 = v00 + u * (v01 - v00);
-        const double u1 = v10 + u * (v11 - v10);
-        val = u0 + v * (u1 - u0);
-      }
-      dst[s * dst_sn + p] = Conv<T>::from_f64(val);
-    }
-  }
-  if (bad) atomicOr(err_flags, XRS_EFLAG_STATE);
-}
 
 // ---- per-tile records + chunk offsets from the K4 accumulators ---------------
 // Mirrors the host tiling (rectify.py:312-419 via base.py:565-629 and
@@ -1088,17 +1147,17 @@ extern "C" int xrs_ij_bboxes(const double* x, const double* y, int64_t h, int64_
   return XRS_OK;
 }
 
-extern "C" int xrs_rectify_ij(const double* x, const double* y, int64_t h, int64_t w,
-                              int64_t sy, const void* tiles, int64_t ntiles, int64_t ntiles_x,
-                              const int64_t* chunk_offsets, int64_t max_chunks,
-                              int64_t dst_h, int64_t dst_w, double x_scale,
-                              double y_scale, double uv_delta, uint32_t* keys, double* ij,
-                              int32_t* err_flags, void* stream) {
-  using namespace xrs;
-  if (!x || !y || !tiles || !keys || !ij || !err_flags || h < 2 || w < 2 || sy < w || ntiles < 1 ||
-      dst_h < 1 || dst_w < 1 || h * w >= (int64_t)UINT32_MAX || !chunk_offsets || max_chunks < 0 ||
-      dst_h > INT32_MAX || dst_w > INT32_MAX) {
-    xrs_set_error("xrs_rectify_ij: invalid argument");
+namespace xrs {
+namespace {
+int rectify_ij_impl(const char* what, const double* x, const double* y, int64_t h, int64_t w,
+                    int64_t sy, const void* tiles, int64_t ntiles, const int64_t* chunk_offsets,
+                    int64_t max_chunks, int64_t dst_h, int64_t dst_w, double x_scale,
+                    double y_scale, double uv_delta, uint32_t* keys, double* ij,
+                    int32_t* err_flags, const FusedVar* fv, int fv_dtype, hipStream_t st) {
+  if (!x || !y || !tiles || !keys || (!ij && !(fv && !fv->write_ij)) || !err_flags || h < 2 ||
+      w < 2 || sy < w || ntiles < 1 || dst_h < 1 || dst_w < 1 || h * w >= (int64_t)UINT32_MAX ||
+      !chunk_offsets || max_chunks < 0 || dst_h > INT32_MAX || dst_w > INT32_MAX) {
+    xrs_set_error("%s: invalid argument", what);
     return XRS_ERR_ARG;
   }
   RectArgs a;
@@ -1117,23 +1176,81 @@ extern "C" int xrs_rectify_ij(const double* x, const double* y, int64_t h, int64
   const int64_t widen = xrs_testing_value(XRS_TESTING_RECTIFY_MARGIN);
   a.margin_scale = widen > 1 ? (float)widen : 1.0f;
   a.narrow = (dst_h * dst_w < ((int64_t)1 << 30) && dst_w < ((int64_t)1 << 24)) ? 1 : 0;
-  hipStream_t st = static_cast<hipStream_t>(stream);
   XRS_HIP_CHECK(hipMemsetAsync(keys, 0xFF, (size_t)(dst_h * dst_w) * sizeof(uint32_t), st));
   {
     // as many blocks as are resident at once (fewer when the caller knows a
     // smaller strip count)
     constexpr int wpb = kClaimThreads / 64;
     static const int resident =   // one device model per process
-        resident_blocks(reinterpret_cast<const void*>(rectify_claim_kernel), kClaimThreads);
+        resident_blocks(reinterpret_cast<const void*>(rectify_claim_kernel<true>),
+                        kClaimThreads);
     const int64_t want = max_chunks > 0 ? (max_chunks + wpb - 1) / wpb : resident;
     const int nb = (int)min(want, (int64_t)resident);
-    hipLaunchKernelGGL(rectify_claim_kernel, dim3(nb), dim3(kClaimThreads), 0, st, a);
+    if (ntiles <= kClaimOffsLds)
+      hipLaunchKernelGGL(rectify_claim_kernel<true>, dim3(nb), dim3(kClaimThreads), 0, st, a);
+    else
+      hipLaunchKernelGGL(rectify_claim_kernel<false>, dim3(nb), dim3(kClaimThreads), 0, st, a);
     XRS_HIP_CHECK(hipGetLastError());
   }
   const int nb2 = grid_blocks(256 * 32, 1, 1 << 24);
-  hipLaunchKernelGGL(rectify_resolve_kernel, dim3(nb2), dim3(kThreads), 0, st, a);
+  if (!fv) {
+    hipLaunchKernelGGL((rectify_resolve_kernel<uint8_t, false>), dim3(nb2), dim3(kThreads), 0,
+                       st, a, FusedVar{});
+  } else {
+    const int rc = dispatch_dtype(fv_dtype, [&](auto tag) -> int {
+      using T = decltype(tag);
+      hipLaunchKernelGGL((rectify_resolve_kernel<T, true>), dim3(nb2), dim3(kThreads), 0, st, a,
+                         *fv);
+      return XRS_OK;
+    });
+    if (rc != XRS_OK) {
+      xrs_set_error("%s: unsupported variable dtype %d", what, fv_dtype);
+      return XRS_ERR_ARG;
+    }
+  }
   XRS_HIP_CHECK(hipGetLastError());
   return XRS_OK;
+}
+}  // namespace
+}  // namespace xrs
+
+extern "C" int xrs_rectify_ij(const double* x, const double* y, int64_t h, int64_t w,
+                              int64_t sy, const void* tiles, int64_t ntiles, int64_t ntiles_x,
+                              const int64_t* chunk_offsets, int64_t max_chunks,
+                              int64_t dst_h, int64_t dst_w, double x_scale,
+                              double y_scale, double uv_delta, uint32_t* keys, double* ij,
+                              int32_t* err_flags, void* stream) {
+  (void)ntiles_x;
+  return xrs::rectify_ij_impl("xrs_rectify_ij", x, y, h, w, sy, tiles, ntiles, chunk_offsets,
+                              max_chunks, dst_h, dst_w, x_scale, y_scale, uv_delta, keys, ij,
+                              err_flags, nullptr, 0, static_cast<hipStream_t>(stream));
+}
+
+extern "C" int xrs_rectify_ij_var(const double* x, const double* y, int64_t h, int64_t w,
+                                  int64_t sy, const void* tiles, int64_t ntiles,
+                                  const int64_t* chunk_offsets, int64_t max_chunks,
+                                  int64_t dst_h, int64_t dst_w, double x_scale, double y_scale,
+                                  double uv_delta, uint32_t* keys, double* ij,
+                                  const void* src, int src_dtype, int64_t n, int64_t src_h,
+                                  int64_t src_w, int64_t src_sn, int64_t src_sy, void* dst,
+                                  int64_t dst_sn, int interp, double fill,
+                                  int32_t* err_flags, void* stream) {
+  using namespace xrs;
+  if (interp != XRS_INTERP_NEAREST && interp != XRS_INTERP_BILINEAR &&
+      interp != XRS_INTERP_TRIANGULAR) {
+    xrs_set_error("interp_methods must be one of 0, 1, 'nearest', 'bilinear', 'triangular'");
+    return XRS_ERR_NOTIMPL;
+  }
+  if (!src || !dst || n < 1 || src_h < 1 || src_w < 1 || src_sy < src_w ||
+      dst_sn < dst_h * dst_w) {
+    xrs_set_error("xrs_rectify_ij_var: invalid argument");
+    return XRS_ERR_ARG;
+  }
+  const FusedVar fv{src, n, src_h, src_w, src_sn, src_sy, dst, dst_sn, fill, interp,
+                    ij != nullptr ? 1 : 0};
+  return rectify_ij_impl("xrs_rectify_ij_var", x, y, h, w, sy, tiles, ntiles, chunk_offsets,
+                         max_chunks, dst_h, dst_w, x_scale, y_scale, uv_delta, keys, ij,
+                         err_flags, &fv, src_dtype, static_cast<hipStream_t>(stream));
 }
 
 extern "C" int xrs_rectify_var(const double* ij, int64_t ij_sn, int64_t dst_h, int64_t dst_w,

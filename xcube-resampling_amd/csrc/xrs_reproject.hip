@@ -51,6 +51,19 @@ constexpr int kPx = 2;                       // columns per thread
 constexpr int kSegW = kThreads * kPx;        // columns per work item
 constexpr int kBand = 32;                    // target rows per work item
 constexpr int kRows = 8;                     // target rows whose loads are in flight together
+
+// K1b's work shape per output width.  float32 out: 512 columns x 32 rows,
+// 8 rows in flight.  float64 out (the reference's bilinear dtype, twice the
+// store bytes): 1024 columns x 8 rows, 4 rows in flight — 6 % faster there
+// and 2 % slower for float32 (A/B interleaved on one box,
+// profiles/r03_k1_shapes_ab.jsonl), so each output width takes its own.
+template <typename O>
+struct K1Shape {
+  static constexpr int px = sizeof(O) == 8 ? 4 : kPx;
+  static constexpr int band = sizeof(O) == 8 ? 8 : kBand;
+  static constexpr int rows = sizeof(O) == 8 ? 4 : kRows;
+  static constexpr int segw = kThreads * px;
+};
 constexpr int kRows2D = 2;                   // K1c: target rows per step (2-D tables; 4: slower)
 
 struct AxisEntry {   // one resolved column (or row) of one tile
@@ -253,6 +266,7 @@ __global__ void __launch_bounds__(kThreads)
 gather_separable_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t bands_per_tile,
                         int64_t segs_per_tile, int64_t nwork) {
   const Geometry& g = a.g;
+  constexpr int kPx = K1Shape<O>::px, kRows = K1Shape<O>::rows;
   const T fill = Conv<T>::from_f64(a.fill);
   for (XcdGroups sl = xcd_groups(nwork, nsegs);; sl.i += sl.step) {
     const int64_t w = sl.item();
@@ -491,9 +505,10 @@ __device__ inline void gather_pixel_any(int mode, const GatherArgs& a, int64_t r
   }
 }
 
-template <int K0, int K1>
+template <int K0, int K1, int FAST>
 __global__ void __launch_bounds__(kThreads)
 gather_proj_kernel(GatherArgs a, XrsProjStep s0, XrsProjStep s1, int mode) {
+  const proj::Pipeline<K0, K1, FAST> pipe(s0, s1);
   // one target pixel per thread and step, grid-stride over the rows of the
   // launch (lanes on consecutive columns): the loop carries almost no state
   // beside the projection's registers (a tile-item loop cost it one wave per
@@ -510,8 +525,7 @@ gather_proj_kernel(GatherArgs a, XrsProjStep s0, XrsProjStep s1, int mode) {
     const uint32_t r = (uint32_t)(p / g.dst_w), c = (uint32_t)(p - (int64_t)r * w32);
     const uint32_t t = (r / th) * ntx + c / tw;
     double px = g.src_x[c], py = g.src_y[r];   // the target pixel centre
-    if constexpr (K0 != 0) proj::apply_step<K0>(s0, px, py);
-    if constexpr (K1 != 0) proj::apply_step<K1>(s1, px, py);
+    pipe(s0, s1, px, py);
     const float x0 = g.tile_x0[t], y0 = g.tile_y0[t];
     const int64_t wi0 = g.tile_win[2 * t], wj0 = g.tile_win[2 * t + 1];
     AxisEntry ex, ey;
@@ -538,7 +552,7 @@ struct Work {
   int64_t ty0, ty1, nsegs, bands_per_tile, segs_per_tile, nwork;
   int nb;
 };
-inline Work work_of(const GatherArgs& a) {
+inline Work work_of(const GatherArgs& a, int64_t band = kBand, int64_t segw = kSegW) {
   const Geometry& g = a.g;
   Work k;
   k.args = a;
@@ -547,8 +561,8 @@ inline Work work_of(const GatherArgs& a) {
   // band height / grid cap: fixed in the product; xrs_testing_set() can change
   // them so the tests cover items that split tiles and the grid-stride loop
   const int64_t band_knob = xrs_testing_value(XRS_TESTING_REPROJECT_BAND);
-  k.args.g.band = band_knob > 0 ? band_knob : kBand;
-  k.args.g.segw = kSegW;
+  k.args.g.band = band_knob > 0 ? band_knob : band;
+  k.args.g.segw = segw;
   k.bands_per_tile = (g.tile_h + k.args.g.band - 1) / k.args.g.band;
   k.segs_per_tile = (g.tile_w + k.args.g.segw - 1) / k.args.g.segw;
   k.nsegs = g.ntiles_x * k.segs_per_tile;
@@ -568,7 +582,7 @@ template <typename T, typename O, int INTERP>
 int launch(const GatherArgs& a, int coord_mode, AxisEntry* xtab, AxisEntry* ytab,
            hipStream_t stream) {
   const Geometry& g = a.g;
-  Work k = work_of(a);
+  Work k = coord_mode == 0 ? work_of(a, K1Shape<O>::band, K1Shape<O>::segw) : work_of(a);
   if (coord_mode == 0) {
     const int64_t ntab = g.ntiles_x * (k.ty1 - k.ty0) * (g.tile_w + g.tile_h);
     const int nbt = grid_blocks(ntab, kThreads, 256 * 8);
@@ -592,8 +606,19 @@ int launch_proj(const GatherArgs& a, const XrsProjStep& s0, const XrsProjStep& s
                 hipStream_t stream) {
   const int64_t np = (a.g.row_end - a.g.row_begin) * a.g.dst_w;
   const int nb = grid_blocks(np, kThreads, 256 * 16);
-  hipLaunchKernelGGL((gather_proj_kernel<K0, K1>), dim3(nb), dim3(kThreads), 0, stream, a, s0,
-                     s1, mode);
+  // the same pipeline code as xrs_transform (proj::fast_kind picks it there too)
+  int fast = proj::kFastNone;
+  if constexpr (K0 == XRS_PROJ_LAEA_INV && K1 == XRS_PROJ_TMERC_FWD)
+    fast = proj::fast_kind(K0, K1, s0);
+  if (fast == proj::kFastObliq)
+    hipLaunchKernelGGL((gather_proj_kernel<K0, K1, proj::kFastObliq>), dim3(nb), dim3(kThreads),
+                       0, stream, a, s0, s1, mode);
+  else if (fast == proj::kFastEquit)
+    hipLaunchKernelGGL((gather_proj_kernel<K0, K1, proj::kFastEquit>), dim3(nb), dim3(kThreads),
+                       0, stream, a, s0, s1, mode);
+  else
+    hipLaunchKernelGGL((gather_proj_kernel<K0, K1, proj::kFastNone>), dim3(nb), dim3(kThreads),
+                       0, stream, a, s0, s1, mode);
   XRS_HIP_CHECK(hipGetLastError());
   return XRS_OK;
 }

@@ -23,16 +23,16 @@ namespace xrs {
 namespace {
 
 constexpr int kThreads = 256;
-using proj::apply_step;
 
 // grid mode: point (r, c) = (x[c], y[r]) (a regular grid's pixel centres,
 // np.meshgrid order); image mode: point p = (x[p], y[p]).  Out row-major.
-// Pipeline = step K0 then step K1 (0: none).
-template <int K0, int K1, bool GRID>
+// Pipeline = step K0 then step K1 (0: none), proj::Pipeline.
+template <int K0, int K1, bool GRID, int FAST>
 __global__ void __launch_bounds__(kThreads)
 transform_kernel(const double* __restrict__ x, const double* __restrict__ y, int64_t w,
                  int64_t h, XrsProjStep s0, XrsProjStep s1, double* __restrict__ out_x,
                  double* __restrict__ out_y) {
+  const proj::Pipeline<K0, K1, FAST> pipe(s0, s1);
   const int64_t n = w * h;
   for (int64_t p = (int64_t)blockIdx.x * kThreads + threadIdx.x; p < n;
        p += (int64_t)gridDim.x * kThreads) {
@@ -45,23 +45,40 @@ transform_kernel(const double* __restrict__ x, const double* __restrict__ y, int
       px = x[p];
       py = y[p];
     }
-    if constexpr (K0 != 0) apply_step<K0>(s0, px, py);
-    if constexpr (K1 != 0) apply_step<K1>(s1, px, py);
+    pipe(s0, s1, px, py);
     out_x[p] = px;
     out_y[p] = py;
   }
+}
+
+template <int K0, int K1, int FAST>
+void launch_fast(bool grid, int nb, hipStream_t st, const double* x, const double* y, int64_t w,
+                 int64_t h, const XrsProjStep& s0, const XrsProjStep& s1, double* ox,
+                 double* oy) {
+  if (grid)
+    hipLaunchKernelGGL((transform_kernel<K0, K1, true, FAST>), dim3(nb), dim3(kThreads), 0, st,
+                       x, y, w, h, s0, s1, ox, oy);
+  else
+    hipLaunchKernelGGL((transform_kernel<K0, K1, false, FAST>), dim3(nb), dim3(kThreads), 0, st,
+                       x, y, w, h, s0, s1, ox, oy);
 }
 
 template <int K0, int K1>
 int launch_pipeline(bool grid, int nb, hipStream_t st, const double* x, const double* y,
                     int64_t w, int64_t h, const XrsProjStep& s0, const XrsProjStep& s1,
                     double* ox, double* oy) {
-  if (grid)
-    hipLaunchKernelGGL((transform_kernel<K0, K1, true>), dim3(nb), dim3(kThreads), 0, st, x, y,
-                       w, h, s0, s1, ox, oy);
-  else
-    hipLaunchKernelGGL((transform_kernel<K0, K1, false>), dim3(nb), dim3(kThreads), 0, st, x, y,
-                       w, h, s0, s1, ox, oy);
+  if constexpr (K0 == XRS_PROJ_LAEA_INV && K1 == XRS_PROJ_TMERC_FWD) {
+    const int fast = proj::fast_kind(K0, K1, s0);
+    if (fast == proj::kFastObliq) {
+      launch_fast<K0, K1, proj::kFastObliq>(grid, nb, st, x, y, w, h, s0, s1, ox, oy);
+      return XRS_OK;
+    }
+    if (fast == proj::kFastEquit) {
+      launch_fast<K0, K1, proj::kFastEquit>(grid, nb, st, x, y, w, h, s0, s1, ox, oy);
+      return XRS_OK;
+    }
+  }
+  launch_fast<K0, K1, proj::kFastNone>(grid, nb, st, x, y, w, h, s0, s1, ox, oy);
   return XRS_OK;
 }
 

@@ -79,8 +79,8 @@ def reproject(src, plan, interp: str, fill: float, out_dtype=None, rows=None, ou
     if out is None:
         out = empty((n, r1 - r0, plan.dst_width), out_dtype, device)
     if plan.fused_transform(device):
-        return _reproject_proj(src, plan, interp_code, fill, out_dtype, r0, r1, out, src_row0,
-                               flags, check, stream)
+        return _reproject_proj(src, h_band, plan, interp_code, fill, out_dtype, r0, r1, out,
+                               src_row0, flags, check, stream)
     tables = plan.device_tables(device)
     lib = _native.lib()
     ws_bytes = lib.xrs_reproject_workspace_size(plan.dst_height, plan.dst_width, plan.tile_height,
@@ -108,13 +108,14 @@ def reproject(src, plan, interp: str, fill: float, out_dtype=None, rows=None, ou
     return out
 
 
-def _reproject_proj(src, plan, interp_code, fill, out_dtype, r0, r1, out, src_row0, flags,
-                    check, stream):
+def _reproject_proj(src, h_band, plan, interp_code, fill, out_dtype, r0, r1, out, src_row0,
+                    flags, check, stream):
     """xrs_reproject_proj: the non-separable plan's transformation fused into
     the gather (reproject.py:472-496 + 268-335 per target pixel, no 2-D
-    coordinate tables)."""
+    coordinate tables).  h_band: the caller's band height (0 for a band that
+    reads no source row; src is then a one-row placeholder, never a row)."""
     device = src.device
-    n, h_band, _ = src.shape
+    n = src.shape[0]
     tabs = plan.device_grid(device)
     steps, nsteps = plan.transformer.device_steps()
     own_flags = flags is None
@@ -242,6 +243,11 @@ def transform(transformer, x, y, grid: bool, device=None, stream=None):
     device = require_device(device if device is not None else getattr(x, "device", None))
     xd = to_device(x, device, np.float64)
     yd = to_device(y, device, np.float64)
+    if stream is not None:
+        # uploads made on the current stream, read on `stream`: keep their
+        # memory out of the allocator's reach until that stream has read it
+        for t in (xd, yd):
+            t.record_stream(stream)
     if grid:
         h, w = yd.numel(), xd.numel()
     else:
@@ -268,21 +274,11 @@ def strip_counts(swin, shin):
     return (nqi + STRIP_W - 1) // STRIP_W * ((nqj + STRIP_H - 1) // STRIP_H)
 
 
-def rectify_ij(x_image, y_image, tiles: np.ndarray, ntiles_x: int, dst_h: int, dst_w: int,
-               x_scale: float, y_scale: float, uv_delta: float, device=None, stream=None,
-               flags: ErrorFlags | None = None):
-    """K5 — per target pixel the fractional source (i, j) (rectify.py:373-576).
-
-    tiles: structured array of TILE_INFO_DTYPE (row-major tile order), or
-    the (tiles, chunk offsets) device pair of rectify_tiles_device.
-    Returns a device tensor (2, dst_h, dst_w) float64 (NaN = no source pixel).
-    An inconsistent tile record or claim key (skipped, never dereferenced)
-    raises; with a caller's ``flags`` the caller checks them (no sync here).
-    """
-    device = require_device(device)
+def _rect_inputs(x_image, y_image, tiles, device):
+    """Device x/y images, tile records, chunk offsets and the strip count
+    of a K5 call (host tiles get their offsets computed here)."""
     x = to_device(x_image, device, np.float64)
     y = to_device(y_image, device, np.float64)
-    h, w = x.shape
     if isinstance(tiles, np.ndarray):   # host tiles: offsets computed here
         tiles = np.ascontiguousarray(tiles, dtype=TILE_INFO_DTYPE)
         nch = np.where(tiles["si0"] >= 0, strip_counts(tiles["swin"], tiles["shin"]), 0)
@@ -293,8 +289,28 @@ def rectify_ij(x_image, y_image, tiles: np.ndarray, ntiles_x: int, dst_h: int, d
     else:                                 # device tiles from rectify_tiles_device
         t_dev, offs = tiles
         ntiles, max_chunks = offs.numel() - 1, 0
+    return x, y, t_dev, offs, ntiles, max_chunks
+
+
+def rectify_ij(x_image, y_image, tiles: np.ndarray, ntiles_x: int, dst_h: int, dst_w: int,
+               x_scale: float, y_scale: float, uv_delta: float, device=None, stream=None,
+               flags: ErrorFlags | None = None, init_nan: bool = False):
+    """K5 — per target pixel the fractional source (i, j) (rectify.py:373-576).
+
+    tiles: structured array of TILE_INFO_DTYPE (row-major tile order), or
+    the (tiles, chunk offsets) device pair of rectify_tiles_device.
+    Returns a device tensor (2, dst_h, dst_w) float64 (NaN = no source pixel).
+    An inconsistent tile record or claim key (skipped, never dereferenced)
+    raises; with a caller's ``flags`` the caller checks them (no sync here).
+    ``init_nan``: the tiles are a subset of the grid (a rank's share,
+    sharding.rectify_shard): pixels of the other tiles are NaN, not garbage.
+    """
+    device = require_device(device)
+    x, y, t_dev, offs, ntiles, max_chunks = _rect_inputs(x_image, y_image, tiles, device)
+    h, w = x.shape
     keys = torch().empty((dst_h, dst_w), dtype=torch().int32, device=device)
-    ij = torch().empty((2, dst_h, dst_w), dtype=torch().float64, device=device)
+    ij = (torch().full((2, dst_h, dst_w), float("nan"), dtype=torch().float64, device=device)
+          if init_nan else torch().empty((2, dst_h, dst_w), dtype=torch().float64, device=device))
     own_flags = flags is None
     if own_flags:
         flags = ErrorFlags(device)
@@ -306,6 +322,45 @@ def rectify_ij(x_image, y_image, tiles: np.ndarray, ntiles_x: int, dst_h: int, d
     if own_flags:
         flags.raise_if_set("xrs_rectify_ij")
     return ij
+
+
+def rectify_ij_var(x_image, y_image, tiles, dst_h: int, dst_w: int, x_scale: float,
+                   y_scale: float, uv_delta: float, src, interp: str, fill,
+                   keep_ij: bool = True, stream=None, flags: ErrorFlags | None = None):
+    """K5 with K6 fused into its resolve pass: the target positions (as
+    rectify_ij) and the first variable ``src`` (n, H, W) sampled at them (as
+    rectify_var) in one pass — the ij image never makes the HBM round trip
+    for that variable.  Returns (ij or None when not ``keep_ij``, out
+    (n, dst_h, dst_w) in src dtype); bit-identical to rectify_ij followed by
+    rectify_var.  The tiles must cover the whole target grid."""
+    device = src.device
+    code = _native.INTERP_CODES.get(interp)
+    if code is None:
+        raise NotImplementedError(
+            f"interp_methods must be one of 0, 1, 'nearest', 'bilinear', "
+            f"'triangular', was '{interp}'.")
+    if src.dim() != 3 or src.stride(2) != 1:
+        raise ValueError("src must be (n, H, W) with contiguous rows")
+    x, y, t_dev, offs, ntiles, max_chunks = _rect_inputs(x_image, y_image, tiles, device)
+    h, w = x.shape
+    n, sh, sw = src.shape
+    keys = torch().empty((dst_h, dst_w), dtype=torch().int32, device=device)
+    ij = (torch().empty((2, dst_h, dst_w), dtype=torch().float64, device=device)
+          if keep_ij else None)
+    out = torch().empty((n, dst_h, dst_w), dtype=src.dtype, device=device)
+    own_flags = flags is None
+    if own_flags:
+        flags = ErrorFlags(device)
+    rc = _native.lib().xrs_rectify_ij_var(
+        ptr(x), ptr(y), h, w, x.stride(0), ptr(t_dev), ntiles, ptr(offs), max_chunks, dst_h,
+        dst_w, float(x_scale), float(y_scale), float(uv_delta), ptr(keys),
+        ptr(ij) if ij is not None else None, ptr(src), _native.DTYPE_CODES[_np_dtype(src)], n,
+        sh, sw, src.stride(0), src.stride(1), ptr(out), out.stride(0), code, float(fill),
+        flags.ptr, stream_handle(device, stream))
+    _native.check(rc, "xrs_rectify_ij_var")
+    if own_flags:
+        flags.raise_if_set("xrs_rectify_ij_var")
+    return ij, out
 
 
 def rectify_var(ij, src, interp: str, fill, stream=None, rows=None, out=None,

@@ -65,7 +65,22 @@ def rectify_dataset(source_ds, target_gm: GridMapping | None = None,
     source_ds, source_gm = _downscale_source_dataset(
         source_ds, source_gm, target_gm, interp_methods, agg_methods, recover_nans)
 
-    target_source_ij = _compute_target_source_ij(source_gm, target_gm, UV_DELTA)
+    yx_dims = (source_gm.xy_dim_names[1], source_gm.xy_dim_names[0])
+    rect_vars = [k for k, v in source_ds.data_vars.items() if v.dims[-2:] == yx_dims]
+    # K6 of the first device-resident variable runs inside K5's resolve pass
+    # (xrs_rectify_ij_var); the ij image is kept only for the others
+    fused = next((k for k in rect_vars if len(source_ds[k].dims) in (2, 3)
+                  and not _streams(source_ds[k].data)), None)
+    if fused is not None:
+        da = source_ds[fused]
+        src = _var_device(da.data)
+        target_source_ij, out = _compute_target_source_ij(
+            source_gm, target_gm, UV_DELTA, var=(
+                src, _get_interp_method_str(interp_methods, fused, da),
+                _get_fill_value(fill_values, fused, da), len(rect_vars) > 1))
+        fused_da = _rectified_array(da, target_gm, out)
+    else:
+        target_source_ij = _compute_target_source_ij(source_gm, target_gm, UV_DELTA)
 
     x_name, y_name = source_gm.xy_var_names
     coords = {k: v for k, v in source_ds.coords.items() if k not in (x_name, y_name)}
@@ -76,11 +91,13 @@ def rectify_dataset(source_ds, target_gm: GridMapping | None = None,
     coords["spatial_ref"] = DataArray(np.array(0), (), target_gm.crs.to_cf())
     target_ds = Dataset(coords=coords, attrs=source_ds.attrs)
 
-    yx_dims = (source_gm.xy_dim_names[1], source_gm.xy_dim_names[0])
     for var_name, data_array in source_ds.data_vars.items():
         if data_array.dims[-2:] == yx_dims:
             assert len(data_array.dims) in (2, 3), \
                 f"Data variable {var_name} has {len(data_array.dims)} dimensions."
+            if var_name == fused:
+                target_ds[var_name] = fused_da
+                continue
             target_ds[var_name] = _rectify_data_array(
                 data_array, var_name, target_gm, target_source_ij, interp_methods, fill_values)
         elif yx_dims[0] not in data_array.dims and yx_dims[1] not in data_array.dims:
@@ -152,6 +169,21 @@ def rectify_tiles(source_gm: GridMapping, target_gm: GridMapping, uv_delta: floa
     else:  # base.py:565-629 on coordinates already resident in HBM
         src_ij_bboxes = kernels.ij_bboxes(xy[0], xy[1], target_gm.xy_bboxes, xy_border, 1,
                                           grid=(len(xs), len(ys)))
+    tiles = tile_records(target_gm, src_ij_bboxes, source_gm.width, source_gm.height)
+    return tiles, len(xs), src_ij_bboxes, xy_border
+
+
+def tile_records(target_gm: GridMapping, src_ij_bboxes, src_w: int, src_h: int) -> np.ndarray:
+    """TILE_INFO records (kernels.py) of the target tiles from their source ij
+    bboxes (rectify.py:391-418; host arithmetic only)."""
+    dst_w, dst_h = target_gm.width, target_gm.height
+    tw, th = target_gm.tile_width, target_gm.tile_height
+    dst_x_min, dst_y_min, dst_x_max, dst_y_max = target_gm.xy_bbox
+    dst_x_res, dst_y_res = target_gm.xy_res
+    j_up = target_gm.is_j_axis_up
+    ys = chunk_sizes(dst_h, th)
+    xs = chunk_sizes(dst_w, tw)
+    src_ij_bboxes = np.asarray(src_ij_bboxes)
     tiles = np.zeros(len(ys) * len(xs), dtype=kernels.TILE_INFO_DTYPE)
     r0s = np.repeat(np.concatenate([[0], np.cumsum(ys)[:-1]]), len(xs))
     c0s = np.tile(np.concatenate([[0], np.cumsum(xs)[:-1]]), len(ys))
@@ -161,19 +193,42 @@ def rectify_tiles(source_gm: GridMapping, target_gm: GridMapping, uv_delta: floa
     none = i_min == -1
     tiles["si0"] = np.where(none, -1, i_min)
     tiles["sj0"] = np.where(none, -1, j_min)
-    tiles["swin"] = np.where(none, 0, np.minimum(i_max + 1, source_gm.width) - i_min)
-    tiles["shin"] = np.where(none, 0, np.minimum(j_max + 1, source_gm.height) - j_min)
+    tiles["swin"] = np.where(none, 0, np.minimum(i_max + 1, src_w) - i_min)
+    tiles["shin"] = np.where(none, 0, np.minimum(j_max + 1, src_h) - j_min)
     # rectify.py:402-406 (python float arithmetic, element by element)
     tiles["x_off"] = [dst_x_min + int(c0) * dst_x_res for c0 in c0s]
     tiles["y_off"] = [(dst_y_min + int(r0) * dst_y_res) if j_up else (dst_y_max - int(r0) * dst_y_res)
                       for r0 in r0s]
-    return tiles, len(xs), src_ij_bboxes, xy_border
+    return tiles
+
+
+def rectify_tile_run(source_gm: GridMapping, target_gm: GridMapping, src, shard, interp: str,
+                     fill, tiles=None, uv_delta: float = UV_DELTA):
+    """One rank's share of a rectification split by ``sharding.rectify_shard``
+    (coordinates and the variable `src` (n, H, W) replicated on every rank):
+    K5 on the rank's run of target tiles, K6 on the target rows they cover.
+    Returns the (n, row1 - row0, W') device band; pixels of tiles the rank
+    does not own are `fill` (``sharding.merge_tile_runs`` assembles the
+    ranks' bands)."""
+    device = require_device(getattr(src, "device", None))
+    xy = source_gm.xy_coords.data
+    xy = (host_to_device(xy[0], device, np.float64), host_to_device(xy[1], device, np.float64))
+    if tiles is None:
+        tiles, _, _, _ = rectify_tiles(source_gm, target_gm, uv_delta, xy=xy)
+    ntx = len(chunk_sizes(target_gm.width, target_gm.tile_width))
+    dst_y_scale = target_gm.y_res if target_gm.is_j_axis_up else -target_gm.y_res
+    run = tiles[shard.tile0:shard.tile1]
+    ij = kernels.rectify_ij(xy[0], xy[1], run, ntx, target_gm.height, target_gm.width,
+                            target_gm.x_res, dst_y_scale, uv_delta, init_nan=True)
+    return kernels.rectify_var(ij, src, interp, fill, rows=shard.rows)
 
 
 def _compute_target_source_ij(source_gm: GridMapping, target_gm: GridMapping,
-                              uv_delta: float):
+                              uv_delta: float, var=None):
     """rectify.py:312-370 -> device tensor (2, H', W') float64 (K5).  The
-    source coordinates are uploaded once and shared by K4 and K5."""
+    source coordinates are uploaded once and shared by K4 and K5.  With
+    ``var=(src, interp, fill, keep_ij)`` the variable is sampled by K5's
+    resolve pass: returns (ij or None, the (n, H', W') rectified variable)."""
     device = require_device()
     xy = source_gm.xy_coords.data
     xy = (host_to_device(xy[0], device, np.float64), host_to_device(xy[1], device, np.float64))
@@ -183,6 +238,11 @@ def _compute_target_source_ij(source_gm: GridMapping, target_gm: GridMapping,
         tiles, ntx, _, _ = rectify_tiles(source_gm, target_gm, uv_delta, xy=xy)
     else:
         ntx = len(chunk_sizes(target_gm.width, target_gm.tile_width))
+    if var is not None:
+        src, interp, fill, keep_ij = var
+        return kernels.rectify_ij_var(xy[0], xy[1], tiles, target_gm.height, target_gm.width,
+                                      target_gm.x_res, dst_y_scale, uv_delta, src, interp, fill,
+                                      keep_ij=keep_ij)
     return kernels.rectify_ij(xy[0], xy[1], tiles, ntx, target_gm.height, target_gm.width,
                               target_gm.x_res, dst_y_scale, uv_delta)
 
@@ -202,24 +262,40 @@ def _device_tiles(source_gm: GridMapping, target_gm: GridMapping, xy):
         (dst_x_min, dst_y_min, dst_y_max), target_gm.xy_res, target_gm.is_j_axis_up)
 
 
+def _streams(data) -> bool:
+    """A numpy variable large enough for the host band pipeline."""
+    return isinstance(data, np.ndarray) and data.ndim in (2, 3) and \
+        data.nbytes >= get_options()["host_streaming_min_bytes"]
+
+
+def _var_device(data):
+    """The variable as a (n, H, W) device tensor."""
+    src = host_to_device(data, require_device())
+    return src.unsqueeze(0) if src.dim() == 2 else src
+
+
 def _rectify_data_array(data_array: DataArray, var_name, target_gm: GridMapping,
                         target_source_ij, interp_methods, fill_values) -> DataArray:
     """rectify.py:263-309 (K6, one launch for all dim-0 slices)."""
     fill_value = _get_fill_value(fill_values, var_name, data_array)
     interp_method = _get_interp_method_str(interp_methods, var_name, data_array)
-    device = require_device()
     data = data_array.data
-    if isinstance(data, np.ndarray) and data.ndim in (2, 3) and \
-            data.nbytes >= get_options()["host_streaming_min_bytes"]:
+    if _streams(data):
         # numpy in, numpy out (rectify.py:297-298): band pipeline
         arr = data.reshape((1,) + data.shape) if data.ndim == 2 else data
-        result = streaming.rectify_host(arr, target_source_ij, interp_method, fill_value, device)
+        out = streaming.rectify_host(arr, target_source_ij, interp_method, fill_value,
+                                     require_device())
     else:
-        src = host_to_device(data, device)
-        if src.dim() == 2:
-            src = src.unsqueeze(0)
-        out = kernels.rectify_var(target_source_ij, src, interp_method, fill_value)
-        result = out if is_device_array(data) else device_to_host(out)
+        out = kernels.rectify_var(target_source_ij, _var_device(data), interp_method,
+                                  fill_value)
+    return _rectified_array(data_array, target_gm, out)
+
+
+def _rectified_array(data_array: DataArray, target_gm: GridMapping, out) -> DataArray:
+    """The (n, H', W') K6 result as the target variable (rectify.py:297-309):
+    numpy in, numpy out; device arrays stay on the device."""
+    data = data_array.data
+    result = device_to_host(out) if is_device_array(out) and not is_device_array(data) else out
     if data.ndim == 2:
         result = result[0]
         dims = (target_gm.xy_dim_names[1], target_gm.xy_dim_names[0])

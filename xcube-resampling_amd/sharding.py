@@ -13,7 +13,17 @@ a raster, so ranks split the work along the two axes that need no exchange:
                      rows or by algorithmic bytes); each rank holds only the
                      source rows its band reads (``ReprojectPlan.
                      source_rows_read``) and writes disjoint target rows —
-                     the bench's partition of config 5 (strong scaling).
+                     the bench's partition of config 5 (strong scaling);
+* ``coarsen_shard`` — the affine / coarsen path (configs 1 and 3): output
+                     chunk rows of ONE array, balanced by output rows; each
+                     rank holds only the source rows its chunks' dask-image
+                     footprints read (the chunk-edge halo included), and runs
+                     the same kernel on them (affine.py:277-313);
+* ``rectify_shard`` — the rectify path (config 4): target tiles dealt as
+                     contiguous raster-order runs balanced by predicted cost
+                     (source quads the claim pass scans + target pixels);
+                     coordinates and variables are replicated per rank, tiles
+                     are independent (rectify.py:347-370, dask.py:41-135).
 
 Collectives appear only around the data path: ``max_over_ranks`` (the bench's
 clock) and ``gather_rows`` (assembling a result on one rank when asked).
@@ -158,6 +168,138 @@ def band_shard(plan, world: int, rank: int, balance: str = "rows",
         return BandShard(rank, world, r0, r0, 0, 0)
     j0, j1 = plan.source_rows_read(r0, r1)
     return BandShard(rank, world, r0, r1, j0, j1)
+
+
+def cost_splits(costs, world: int) -> list[int]:
+    """Boundaries 0 = b_0 <= ... <= b_world = n of `world` contiguous runs of
+    the n work units with (as nearly as unit granularity allows) equal summed
+    cost."""
+    if world < 1:
+        raise ValueError(f"invalid world size {world}")
+    c = np.concatenate([[0.0], np.cumsum(np.asarray(costs, np.float64))])
+    n = len(c) - 1
+    if c[-1] <= 0:
+        return [balanced_range(n, world, r)[0] for r in range(world)] + [n]
+    out = [0]
+    for target in c[-1] * np.arange(1, world) / world:
+        k = int(np.searchsorted(c, target, side="left"))   # nearest boundary to the target
+        if k > 0 and (k > n or target - c[k - 1] <= c[k] - target):
+            k -= 1
+        out.append(min(max(k, out[-1]), n))
+    return out + [n]
+
+
+# ---- affine / coarsen (configs 1 and 3) ------------------------------------------
+@dataclass(frozen=True)
+class CoarsenShard:
+    rank: int
+    world: int
+    chunk0: int     # output y-chunks [chunk0, chunk1)
+    chunk1: int
+    row0: int       # output rows [row0, row1)
+    row1: int
+    src_row0: int   # source rows [src_row0, src_row1) their footprints read
+    src_row1: int
+    plan: object    # the AffinePlan restricted to the chunks, source rows re-based to src_row0
+
+    @property
+    def rows(self) -> tuple[int, int]:
+        return self.row0, self.row1
+
+    @property
+    def src_rows(self) -> tuple[int, int]:
+        return self.src_row0, self.src_row1
+
+
+def coarsen_shard(plan, world: int, rank: int) -> CoarsenShard:
+    """Output chunk rows of `rank` for an affine / coarsen plan
+    (``affine.plan_affine``) split over `world` ranks, balanced by output rows.
+    Every output pixel depends only on its chunk's dask-image input slice
+    (affine.py:336-343: rows [rel_y, rel_y + len_y), which already carries the
+    chunk-edge halo the order-1 taps and the NaN dilation of the coarsen need),
+    so a rank runs the unchanged kernel on the source rows of its chunks:
+    the plan's rel_y is re-based to the first of them.  Plans with a separate
+    coarsen pass (median, mode, std, var) or chunks that do not hold whole
+    coarsen windows are not split (NotImplementedError)."""
+    import dataclasses
+
+    if not 0 <= rank < world:
+        raise ValueError(f"invalid rank {rank} for world size {world}")
+    if plan.post_agg is not None or plan.chunk_y % plan.div_y != 0:
+        raise NotImplementedError("this affine plan cannot be split into output row bands")
+    nchunks = len(plan.rel_y)
+    rows_per_chunk = plan.chunk_y // plan.div_y
+    rows = [min(plan.out_h, (k + 1) * rows_per_chunk) - k * rows_per_chunk
+            for k in range(nchunks)]
+    cuts = cost_splits(rows, world)
+    k0, k1 = cuts[rank], cuts[rank + 1]
+    r0 = k0 * rows_per_chunk
+    r1 = min(plan.out_h, k1 * rows_per_chunk) if k1 > k0 else r0
+    if k1 <= k0:
+        return CoarsenShard(rank, world, k0, k0, r0, r0, 0, 0, None)
+    rel, ln = plan.rel_y[k0:k1], plan.len_y[k0:k1]
+    j0, j1 = int(rel.min()), int((rel + ln).max())
+    sub = dataclasses.replace(plan, out_h=r1 - r0, rel_y=(rel - j0).astype(plan.rel_y.dtype),
+                              len_y=ln, off_y=plan.off_y[k0:k1], _cache={})
+    return CoarsenShard(rank, world, k0, k1, r0, r1, j0, j1, sub)
+
+
+# ---- rectify (config 4) ----------------------------------------------------------
+# predicted K5 + K6 cost of a target tile, in target-pixel units: one source
+# quad scanned by the claim pass costs about RECT_QUAD_WEIGHT target pixels of
+# resolve + sampling (config 4, round 2: claim 0.60 ms for 19.2 M quads,
+# resolve + K6 0.51 ms for 44.6 M pixels)
+RECT_QUAD_WEIGHT = 2.7
+
+
+def rectify_tile_costs(tiles) -> np.ndarray:
+    """Predicted cost of every target tile (TILE_INFO records, kernels.py)."""
+    quads = np.where(tiles["si0"] >= 0,
+                     np.maximum(tiles["swin"].astype(np.int64) - 1, 0) *
+                     np.maximum(tiles["shin"].astype(np.int64) - 1, 0), 0)
+    return RECT_QUAD_WEIGHT * quads + tiles["th"].astype(np.int64) * tiles["tw"]
+
+
+@dataclass(frozen=True)
+class RectifyShard:
+    rank: int
+    world: int
+    tile0: int      # target tiles [tile0, tile1) in raster (row-major) order
+    tile1: int
+    row0: int       # target rows [row0, row1) those tiles cover
+    row1: int
+
+    @property
+    def rows(self) -> tuple[int, int]:
+        return self.row0, self.row1
+
+
+def rectify_shard(tiles, world: int, rank: int) -> RectifyShard:
+    """The contiguous run of target tiles `rank` rectifies (``cost_splits``
+    over ``rectify_tile_costs``).  Tiles are independent (each reads only its
+    source bbox and writes only its pixels), so no exchange is needed."""
+    if not 0 <= rank < world:
+        raise ValueError(f"invalid rank {rank} for world size {world}")
+    cuts = cost_splits(rectify_tile_costs(tiles), world)
+    t0, t1 = cuts[rank], cuts[rank + 1]
+    if t1 <= t0:
+        return RectifyShard(rank, world, t0, t0, 0, 0)
+    r0 = int(tiles["r0"][t0])
+    r1 = int((tiles["r0"][t0:t1] + tiles["th"][t0:t1]).max())
+    return RectifyShard(rank, world, t0, t1, r0, r1)
+
+
+def merge_tile_runs(parts, tiles, dst_shape, fill):
+    """Assemble per-rank rectify results: part = (shard, band (n, r1-r0, W));
+    each tile's pixels come from the rank that owns it."""
+    n = parts[0][1].shape[0] if parts else 1
+    out = np.full((n,) + tuple(dst_shape), fill, dtype=parts[0][1].dtype if parts else float)
+    for shard, band in parts:
+        for t in range(shard.tile0, shard.tile1):
+            r, c = int(tiles["r0"][t]), int(tiles["c0"][t])
+            th, tw = int(tiles["th"][t]), int(tiles["tw"][t])
+            out[:, r:r + th, c:c + tw] = band[:, r - shard.row0:r - shard.row0 + th, c:c + tw]
+    return out
 
 
 def env_rank() -> tuple[int, int, int]:
