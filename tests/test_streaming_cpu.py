@@ -55,26 +55,40 @@ def test_source_rows_copies_only_missing_runs():
     from xcube_resampling_amd import streaming
 
     calls = []
-    orig = streaming._copy
-    streaming._copy = lambda dst, src, nbytes, stream: calls.append(nbytes)
-    try:
-        class _Dev:   # stand-in device buffer: only data_ptr() is used
-            def __getitem__(self, idx):
-                return type("R", (), {"data_ptr": lambda self: 0})()
 
-        src = np.zeros((2, 100, 8), np.float32)
-        rows = streaming._SourceRows(src, _Dev(), None)
-        rows.need(40, 60)
-        rows.need(10, 50)        # rows 10..39 missing -> one run
-        rows.need(55, 70)        # rows 60..69
-        rows.need(-5, 5)         # clipped to 0..4
-        rows.need(30, 20)        # empty
-    finally:
-        streaming._copy = orig
+    class _Dev:   # stand-in device buffer: only data_ptr() is used
+        def __getitem__(self, idx):
+            return type("R", (), {"data_ptr": lambda self: 0})()
+
+    class _Stage:  # stand-in staging: records the host runs handed to it
+        def h2d(self, dst_ptr, src, stream):
+            assert src.flags.c_contiguous
+            calls.append(src.nbytes)
+
+    src = np.zeros((2, 100, 8), np.float32)
+    rows = streaming._SourceRows(src, _Dev(), None, _Stage())
+    rows.need(40, 60)
+    rows.need(10, 50)        # rows 10..39 missing -> one run
+    rows.need(55, 70)        # rows 60..69
+    rows.need(-5, 5)         # clipped to 0..4
+    rows.need(30, 20)        # empty
     row = 8 * 4
     assert calls == [20 * row] * 2 + [30 * row] * 2 + [10 * row] * 2 + [5 * row] * 2
     assert rows.resident[0:5].all() and rows.resident[10:70].all()
     assert not rows.resident[5:10].any() and not rows.resident[70:].any()
+
+
+def test_host_copy_parts_cover_the_array():
+    """The staging copies split large arrays over a thread pool in parts:
+    every byte lands once, sizes above and below one part, odd lengths."""
+    from xcube_resampling_amd import streaming
+
+    rng = np.random.default_rng(0)
+    for n in (0, 7, streaming._COPY_PART, 3 * streaming._COPY_PART + 12345):
+        src = rng.integers(0, 256, n, dtype=np.uint8)
+        dst = np.zeros(n, np.uint8)
+        streaming._host_copy(dst, src)
+        assert np.array_equal(dst, src)
 
 
 def test_band_rows_multiple_of_unit():

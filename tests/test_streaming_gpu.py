@@ -96,8 +96,9 @@ def test_streamed_errors():
 
 def test_pinned_transfers_in_affine_and_rectify_paths():
     """The dataset APIs move numpy arrays of at least host_streaming_min_bytes
-    by DMA from page-locked memory (streaming.host_to_device / device_to_host):
-    same bits as the small-array path."""
+    through the page-locked staging buffers (streaming.host_to_device /
+    device_to_host, several staging chunks at the sizes below): same bits as
+    the small-array path."""
     import xcube_resampling_amd as xrs
 
     rng = np.random.default_rng(5)
@@ -131,9 +132,8 @@ def test_pinned_transfers_in_affine_and_rectify_paths():
 
 
 def test_streamed_from_read_only_memmap(tmp_path):
-    """A file-backed, read-only source (np.load(mmap_mode='r')): page-locking
-    may be refused; the copies then go through the runtime's staging — same
-    bits either way."""
+    """A file-backed, read-only source (np.load(mmap_mode='r')) streams
+    through the staging buffers like any array — same bits."""
     from xcube_resampling_amd import streaming
 
     g = load_golden("reproject_f32.npz")

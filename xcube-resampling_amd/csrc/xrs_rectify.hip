@@ -935,7 +935,89 @@ struct FusedVar {
   int write_ij;    // 0: the ij image is not needed by any other variable
 };
 
-template <typename T, bool FUSE>
+// K6 of R target pixels (rows p0 + r * pstride) in one batch: positions
+// classified, then the taps of every row requested before any is used, then
+// the values — sample_px's arithmetic, with R rows' gathers in flight at once
+// instead of one dependent chain per row.
+template <typename T, int INTERP, int R>
+__device__ inline void sample_rows(const double* fi, const double* fj, int nr,
+                                   const FusedVar& fv, const T* __restrict__ src,
+                                   T* __restrict__ dst, int64_t p0, int64_t pstride, T tfill,
+                                   bool& bad) {
+  // tap rows / columns as int32 (src_h, src_w < 2^31: checked at launch);
+  // the 64-bit offsets are formed at the loads
+  int32_t ti0[R], ti1[R], tj0[R], tj1[R];
+  double u[R], v[R];
+  bool ok[R];
+  const int64_t imax = fv.src_w - 1, jmax = fv.src_h - 1;
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    ok[r] = false;
+    ti0[r] = ti1[r] = tj0[r] = tj1[r] = 0;
+    u[r] = v[r] = 0.0;
+    if (r >= nr || fi[r] != fi[r] || fj[r] != fj[r]) continue;
+    if (!(fi[r] >= 0.0 && fi[r] < (double)fv.src_w && fj[r] >= 0.0 && fj[r] < (double)fv.src_h)) {
+      bad = true;
+      continue;
+    }
+    int64_t i0 = (int64_t)fi[r], j0 = (int64_t)fj[r];   // int() truncation (values >= 0)
+    u[r] = fi[r] - (double)i0;
+    v[r] = fj[r] - (double)j0;
+    ok[r] = true;
+    if (INTERP == XRS_INTERP_NEAREST) {
+      if (u[r] > 0.5) i0 = min(max(i0 + 1, (int64_t)0), imax);
+      if (v[r] > 0.5) j0 = min(max(j0 + 1, (int64_t)0), jmax);
+    } else {
+      ti1[r] = (int32_t)min(max(i0 + 1, (int64_t)0), imax);
+      tj1[r] = (int32_t)min(max(j0 + 1, (int64_t)0), jmax);
+    }
+    ti0[r] = (int32_t)i0;
+    tj0[r] = (int32_t)j0;
+  }
+  for (int64_t s = 0; s < fv.n; ++s) {
+    const T* S = src + s * fv.src_sn;
+    T t00[R], t01[R], t10[R], t11[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {   // rows without a sample read element 0
+      const T* s0 = S + (int64_t)tj0[r] * fv.src_sy;
+      t00[r] = s0[ti0[r]];
+      if (INTERP != XRS_INTERP_NEAREST) {
+        const T* s1 = S + (int64_t)tj1[r] * fv.src_sy;
+        t01[r] = s0[ti1[r]];
+        t10[r] = s1[ti0[r]];
+        t11[r] = s1[ti1[r]];
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if (r >= nr) break;
+      T out = tfill;
+      if (ok[r]) {
+        if (INTERP == XRS_INTERP_NEAREST) {
+          out = t00[r];
+        } else {
+          const double v00 = (double)t00[r], v01 = (double)t01[r];
+          const double v10 = (double)t10[r], v11 = (double)t11[r];
+          double val;
+          if (INTERP == XRS_INTERP_TRIANGULAR) {
+            if (u[r] + v[r] < 1.0)
+              val = v00 + u[r] * (v01 - v00) + v[r] * (v10 - v00);
+            else
+              val = v11 + (1.0 - u[r]) * (v10 - v11) + (1.0 - v[r]) * (v01 - v11);
+          } else {
+            const double u0 = v00 + u[r] * (v01 - v00);
+            const double u1 = v10 + u[r] * (v11 - v10);
+            val = u0 + v[r] * (u1 - u0);
+          }
+          out = Conv<T>::from_f64(val);
+        }
+      }
+      dst[s * fv.dst_sn + p0 + r * pstride] = out;
+    }
+  }
+}
+
+template <typename T, bool FUSE, int INTERP>
 __global__ void __launch_bounds__(kThreads)
 rectify_resolve_kernel(RectArgs a, FusedVar fv) {
   const int64_t n = a.dst_h * a.dst_w;
@@ -981,8 +1063,11 @@ rectify_resolve_kernel(RectArgs a, FusedVar fv) {
           Q[r] = load_quad(a, qj[r], qi[r]);
         }
       }
+      double fi[kResolveRows], fj[kResolveRows];   // the rows' source positions
 #pragma unroll
       for (int r = 0; r < kResolveRows; ++r) {
+        fi[r] = NAN;
+        fj[r] = NAN;
         if (r >= nr) break;
         double oi = NAN, oj = NAN;
         if (key[r] != 0xFFFFFFFFu) {
@@ -1012,20 +1097,15 @@ rectify_resolve_kernel(RectArgs a, FusedVar fv) {
           a.ij[p] = oi;
           a.ij[n + p] = oj;
         }
-        if constexpr (FUSE) {
-          const T* src = static_cast<const T*>(fv.src);
-          T* dst = static_cast<T*>(fv.dst);
-          if (fv.interp == XRS_INTERP_NEAREST)
-            sample_px<T, XRS_INTERP_NEAREST>(oi, oj, src, fv.n, fv.src_h, fv.src_w, fv.src_sn,
-                                             fv.src_sy, dst, fv.dst_sn, p, tfill, bad);
-          else if (fv.interp == XRS_INTERP_TRIANGULAR)
-            sample_px<T, XRS_INTERP_TRIANGULAR>(oi, oj, src, fv.n, fv.src_h, fv.src_w,
-                                                fv.src_sn, fv.src_sy, dst, fv.dst_sn, p, tfill,
-                                                bad);
-          else
-            sample_px<T, XRS_INTERP_BILINEAR>(oi, oj, src, fv.n, fv.src_h, fv.src_w, fv.src_sn,
-                                              fv.src_sy, dst, fv.dst_sn, p, tfill, bad);
-        }
+        fi[r] = oi;
+        fj[r] = oj;
+      }
+      if constexpr (FUSE) {
+        // the rows' samples: every row's taps in flight together
+        const T* src = static_cast<const T*>(fv.src);
+        T* dst = static_cast<T*>(fv.dst);
+        sample_rows<T, INTERP, kResolveRows>(fi, fj, nr, fv, src, dst, p0, a.dst_w, tfill,
+                                             bad);
       }
     }
   }
@@ -1194,13 +1274,20 @@ int rectify_ij_impl(const char* what, const double* x, const double* y, int64_t 
   }
   const int nb2 = grid_blocks(256 * 32, 1, 1 << 24);
   if (!fv) {
-    hipLaunchKernelGGL((rectify_resolve_kernel<uint8_t, false>), dim3(nb2), dim3(kThreads), 0,
-                       st, a, FusedVar{});
+    hipLaunchKernelGGL((rectify_resolve_kernel<uint8_t, false, XRS_INTERP_NEAREST>), dim3(nb2),
+                       dim3(kThreads), 0, st, a, FusedVar{});
   } else {
     const int rc = dispatch_dtype(fv_dtype, [&](auto tag) -> int {
       using T = decltype(tag);
-      hipLaunchKernelGGL((rectify_resolve_kernel<T, true>), dim3(nb2), dim3(kThreads), 0, st, a,
-                         *fv);
+      if (fv->interp == XRS_INTERP_NEAREST)
+        hipLaunchKernelGGL((rectify_resolve_kernel<T, true, XRS_INTERP_NEAREST>), dim3(nb2),
+                           dim3(kThreads), 0, st, a, *fv);
+      else if (fv->interp == XRS_INTERP_TRIANGULAR)
+        hipLaunchKernelGGL((rectify_resolve_kernel<T, true, XRS_INTERP_TRIANGULAR>), dim3(nb2),
+                           dim3(kThreads), 0, st, a, *fv);
+      else
+        hipLaunchKernelGGL((rectify_resolve_kernel<T, true, XRS_INTERP_BILINEAR>), dim3(nb2),
+                           dim3(kThreads), 0, st, a, *fv);
       return XRS_OK;
     });
     if (rc != XRS_OK) {
@@ -1242,7 +1329,7 @@ extern "C" int xrs_rectify_ij_var(const double* x, const double* y, int64_t h, i
     return XRS_ERR_NOTIMPL;
   }
   if (!src || !dst || n < 1 || src_h < 1 || src_w < 1 || src_sy < src_w ||
-      dst_sn < dst_h * dst_w) {
+      dst_sn < dst_h * dst_w || src_h > INT32_MAX || src_w > INT32_MAX) {
     xrs_set_error("xrs_rectify_ij_var: invalid argument");
     return XRS_ERR_ARG;
   }

@@ -3,9 +3,10 @@
 The reference takes numpy arrays and returns computed numpy arrays
 (reproject.py:208-213, 254-255).  A device round trip of a whole raster
 through pageable memory serialises three steps that each take far longer than
-the kernel (40960^2 f32: 6.7 GB in, 6.7 GB out, ~2.6 ms of K1).  Here the
-source and result arrays are page-locked in place (``xrs_host_register``) and
-the target is processed in bands of target rows on three HIP streams:
+the kernel (40960^2 f32: 6.7 GB in, 6.7 GB out, ~2.6 ms of K1).  Here every
+host <-> device copy goes through two page-locked staging buffers (the host
+copies one chunk while the DMA engine moves the other, `_Staging`) and the
+target is processed in bands of target rows on three HIP streams:
 
     copy-in  : source rows a band needs that are not yet resident -> HBM
     kernel   : K1 over the band's target rows (waits for its rows)
@@ -29,48 +30,121 @@ from .device import empty, numpy_dtype, require_device, stream_handle, to_device
 from .options import get_options
 
 
-class HostPin:
-    """Page-lock a C-contiguous numpy array in place for the lifetime of the
-    context (no copy).  Memory that is already registered stays as it is;
-    memory the runtime refuses to lock (e.g. a file-backed np.memmap) stays
-    pageable — the copies are then staged by the runtime: slower, same bytes."""
-
-    def __init__(self, array: np.ndarray):
-        if not array.flags.c_contiguous:
-            raise ValueError("HostPin needs a C-contiguous array")
-        self.array = array
-        self._registered = False
-
-    def __enter__(self):
-        if self.array.nbytes:
-            rc = _native.lib().xrs_host_register(
-                ctypes.c_void_p(self.array.ctypes.data), self.array.nbytes)
-            if rc == _native.XRS_ERR_ARG:
-                _native.check(rc, "xrs_host_register")
-            if rc == _native.XRS_ERR_HIP:
-                LOG.debug("host array not page-locked (%s); copies are staged",
-                          _native.last_error())
-            self._registered = rc == _native.XRS_OK
-        return self.array
-
-    def __exit__(self, *exc):
-        if self._registered:
-            self._registered = False
-            _native.check(_native.lib().xrs_host_unregister(
-                ctypes.c_void_p(self.array.ctypes.data)), "xrs_host_unregister")
-        return False
-
-
 def _copy(dst_ptr: int, src_ptr: int, nbytes: int, stream) -> None:
     rc = _native.lib().xrs_copy_async(ctypes.c_void_p(dst_ptr), ctypes.c_void_p(src_ptr),
                                       int(nbytes), stream_handle(stream=stream))
     _native.check(rc, "xrs_copy_async")
 
 
+_STAGE_BYTES = 16 << 20     # one staging buffer
+_COPY_PART = 2 << 20        # host copies are split over threads in parts of this size
+_COPY_POOL = None
+
+
+def _host_copy(dst: np.ndarray, src: np.ndarray) -> None:
+    """dst[:] = src for flat uint8 views, over a small thread pool (numpy's
+    contiguous copy releases the GIL): the staging copies run at several
+    times one thread's memcpy rate."""
+    global _COPY_POOL
+    n = dst.size
+    if n <= _COPY_PART:
+        dst[:] = src
+        return
+    if _COPY_POOL is None:
+        from concurrent.futures import ThreadPoolExecutor
+        _COPY_POOL = ThreadPoolExecutor(max_workers=8, thread_name_prefix="xrs-stage")
+    parts = [(o, min(n, o + _COPY_PART)) for o in range(0, n, _COPY_PART)]
+
+    def one(p):
+        dst[p[0]:p[1]] = src[p[0]:p[1]]
+
+    list(_COPY_POOL.map(one, parts))
+
+
+class _Staging:
+    """Two page-locked host buffers (torch's pinned allocator: allocated once
+    per process, never registered / unregistered per call) through which the
+    streamed host <-> device copies go: the host copies a chunk into (out of)
+    one buffer while the DMA engine moves the other.  Arrays of the caller
+    are never page-locked in place: after hipHostRegister / hipHostUnregister
+    of arrays the caller then freed, a later pageable copy from a new array
+    faulted with an illegal address (twice in the GPU suite, at the first
+    copy after such a sequence) — staging removes that pattern."""
+
+    def __init__(self):
+        t = torch()
+        self.bufs = [t.empty(_STAGE_BYTES, dtype=t.uint8, pin_memory=True) for _ in range(2)]
+        self.views = [b.numpy() for b in self.bufs]
+        self.events = [None, None]   # the last DMA that used each buffer
+        self.k = 0
+
+    def _take(self) -> int:
+        i, self.k = self.k, self.k ^ 1
+        if self.events[i] is not None:
+            self.events[i].synchronize()
+            self.events[i] = None
+        return i
+
+    def _record(self, i: int, stream) -> None:
+        ev = torch().cuda.Event()
+        ev.record(stream)
+        self.events[i] = ev
+
+    def h2d(self, dst_ptr: int, src: np.ndarray, stream) -> None:
+        """C-contiguous host array -> device bytes at dst_ptr, on `stream`.
+        Returns once every chunk is queued (a buffer is refilled only after
+        its previous DMA has completed)."""
+        flat = np.ascontiguousarray(src).reshape(-1).view(np.uint8)
+        for off in range(0, flat.size, _STAGE_BYTES):
+            nb = min(_STAGE_BYTES, flat.size - off)
+            i = self._take()
+            _host_copy(self.views[i][:nb], flat[off:off + nb])
+            _copy(dst_ptr + off, self.bufs[i].data_ptr(), nb, stream)
+            self._record(i, stream)
+
+    def d2h(self, dst: np.ndarray, src_ptr: int, stream) -> None:
+        """Device bytes at src_ptr -> C-contiguous host array `dst`, on
+        `stream`; returns when they have landed in `dst`."""
+        flat = dst.reshape(-1).view(np.uint8)
+        pending = None
+        for off in range(0, flat.size, _STAGE_BYTES):
+            nb = min(_STAGE_BYTES, flat.size - off)
+            i = self._take()
+            _copy(self.bufs[i].data_ptr(), src_ptr + off, nb, stream)
+            self._record(i, stream)
+            if pending is not None:
+                self._drain(flat, *pending)
+            pending = (i, off, nb)
+        if pending is not None:
+            self._drain(flat, *pending)
+
+    def _drain(self, flat: np.ndarray, i: int, off: int, nb: int) -> None:
+        self.events[i].synchronize()
+        self.events[i] = None
+        _host_copy(flat[off:off + nb], self.views[i][:nb])
+
+    def drain(self) -> None:
+        """Wait for every DMA still using a buffer."""
+        for i in range(2):
+            if self.events[i] is not None:
+                self.events[i].synchronize()
+                self.events[i] = None
+
+
+_STAGING = None
+
+
+def _staging() -> _Staging:
+    global _STAGING
+    if _STAGING is None:
+        _STAGING = _Staging()
+    return _STAGING
+
+
 def host_to_device(arr, device, dtype=None):
     """numpy -> device tensor.  Arrays of at least ``host_streaming_min_bytes``
-    are page-locked in place and copied by DMA (no pageable staging copy);
-    smaller ones take torch's copy."""
+    go through the page-locked staging buffers (DMA overlapped with the host
+    copy); smaller ones take torch's copy."""
     if not isinstance(arr, np.ndarray):
         return to_device(arr, device, dtype)
     arr = np.ascontiguousarray(arr if dtype is None else arr.astype(dtype, copy=False))
@@ -79,28 +153,27 @@ def host_to_device(arr, device, dtype=None):
         return to_device(arr, device)
     dst = empty(arr.shape, arr.dtype, device)
     stream = torch().cuda.current_stream(device)
-    with HostPin(arr):
-        try:
-            _copy(dst.data_ptr(), arr.ctypes.data, arr.nbytes, stream)
-        finally:   # the copy has landed before the array is unpinned
-            stream.synchronize()
+    st = _staging()
+    try:
+        st.h2d(dst.data_ptr(), arr, stream)
+    finally:
+        st.drain()
     return dst
 
 
 def device_to_host(x) -> np.ndarray:
-    """device tensor -> numpy, by DMA into a page-locked result for tensors of
-    at least ``host_streaming_min_bytes``."""
+    """device tensor -> numpy through the page-locked staging buffers, for
+    tensors of at least ``host_streaming_min_bytes``."""
     nbytes = x.numel() * x.element_size()
     if nbytes < max(1, get_options()["host_streaming_min_bytes"]):
         return x.cpu().numpy()
     x = x.contiguous()
     out = np.empty(tuple(x.shape), numpy_dtype(x.dtype))
-    stream = torch().cuda.current_stream(x.device)
-    with HostPin(out):
-        try:
-            _copy(out.ctypes.data, x.data_ptr(), nbytes, stream)
-        finally:
-            stream.synchronize()
+    st = _staging()
+    try:
+        st.d2h(out, x.data_ptr(), torch().cuda.current_stream(x.device))
+    finally:
+        st.drain()
     return out
 
 
@@ -169,39 +242,46 @@ def reproject_host(src: np.ndarray, plan, interp: str, fill: float, out_dtype=No
         plan.device_tables(device)
     for s in (s_in, s_k, s_out):
         s.wait_stream(cur)
-    row_src, row_dst = w * src.itemsize, wd * out_dtype.itemsize
-    freed: list = [None, None]
-    with HostPin(src), HostPin(out):
-        try:
-            hi = 0
-            for b, ((r0, r1), (_, j1)) in enumerate(zip(bands, src_rows)):
-                if j1 > hi:   # rows [hi, j1) of every slice (contiguous per slice)
-                    for s in range(n):
-                        _copy(dsrc[s, hi].data_ptr(), src[s, hi:j1].ctypes.data,
-                              (j1 - hi) * row_src, s_in)
-                    hi = j1
-                ev_in = t.cuda.Event()
-                ev_in.record(s_in)
-                s_k.wait_event(ev_in)
-                if freed[b % 2] is not None:   # the copy-out of band b-2 has drained
-                    s_k.wait_event(freed[b % 2])
-                buf = bufs[b % 2][:, :r1 - r0]
-                kernels.reproject(dsrc, plan, interp, fill, out_dtype=out_dtype, rows=(r0, r1),
-                                  out=buf, flags=flags, stream=s_k)
-                ev_k = t.cuda.Event()
-                ev_k.record(s_k)
-                s_out.wait_event(ev_k)
+    st = _staging()
+    prev = None   # the band whose copy-out is pending: it overlaps the next kernel
+    try:
+        hi = 0
+        for b, ((r0, r1), (_, j1)) in enumerate(zip(bands, src_rows)):
+            if j1 > hi:   # rows [hi, j1) of every slice (contiguous per slice)
                 for s in range(n):
-                    _copy(out[s, r0:r1].ctypes.data, buf[s].data_ptr(), (r1 - r0) * row_dst,
-                          s_out)
-                freed[b % 2] = t.cuda.Event()
-                freed[b % 2].record(s_out)
-        finally:   # never unpin (or free) while a copy may still be in flight
-            s_in.synchronize()
-            s_k.synchronize()
-            s_out.synchronize()
+                    st.h2d(dsrc[s, hi].data_ptr(), src[s, hi:j1], s_in)
+                hi = j1
+            ev_in = t.cuda.Event()
+            ev_in.record(s_in)
+            s_k.wait_event(ev_in)
+            # bufs[b % 2] held band b - 2, whose copy-out has landed (d2h returns
+            # when the bytes are in `out`)
+            buf = bufs[b % 2][:, :r1 - r0]
+            kernels.reproject(dsrc, plan, interp, fill, out_dtype=out_dtype, rows=(r0, r1),
+                              out=buf, flags=flags, stream=s_k)
+            ev_k = t.cuda.Event()
+            ev_k.record(s_k)
+            if prev is not None:
+                _copy_out(st, out, prev, s_out)
+            prev = (r0, r1, buf, ev_k)
+        if prev is not None:
+            _copy_out(st, out, prev, s_out)
+    finally:   # nothing may still use the device buffers when they are freed
+        st.drain()
+        s_in.synchronize()
+        s_k.synchronize()
+        s_out.synchronize()
     flags.raise_if_set("reproject")
     return out
+
+
+def _copy_out(st: _Staging, out: np.ndarray, band, s_out) -> None:
+    """The result rows [r0, r1) of every slice: device band buffer -> `out`,
+    after the band's kernel (event ev_k)."""
+    r0, r1, buf, ev_k = band
+    s_out.wait_event(ev_k)
+    for s in range(out.shape[0]):
+        st.d2h(out[s, r0:r1], buf[s].data_ptr(), s_out)
 
 
 # ---- generic band pipeline (affine / rectify host paths) --------------------------
@@ -209,10 +289,9 @@ class _SourceRows:
     """Host -> device copies of source rows on demand: only rows not yet
     resident are copied (in contiguous runs, every dim-0 slice), on `stream`."""
 
-    def __init__(self, src: np.ndarray, dsrc, stream):
-        self.src, self.dsrc, self.stream = src, dsrc, stream
+    def __init__(self, src: np.ndarray, dsrc, stream, staging: _Staging):
+        self.src, self.dsrc, self.stream, self.staging = src, dsrc, stream, staging
         self.resident = np.zeros(src.shape[1], bool)
-        self.row_bytes = src.shape[2] * src.itemsize
 
     def need(self, j0: int, j1: int) -> None:
         j0, j1 = max(0, int(j0)), min(len(self.resident), int(j1))
@@ -223,8 +302,7 @@ class _SourceRows:
         for a, b in zip(edges[0::2], edges[1::2]):
             ra, rb = j0 + int(a), j0 + int(b)
             for s in range(self.src.shape[0]):
-                _copy(self.dsrc[s, ra].data_ptr(), self.src[s, ra:rb].ctypes.data,
-                      (rb - ra) * self.row_bytes, self.stream)
+                self.staging.h2d(self.dsrc[s, ra].data_ptr(), self.src[s, ra:rb], self.stream)
         self.resident[j0:j1] = True
 
 
@@ -237,8 +315,8 @@ def band_pipeline(src: np.ndarray, dsrc, out: np.ndarray, bands, src_rows, launc
         kernel   : launch(b, r0, r1, buf, stream) writes the band into buf
         copy-out : buf -> out[:, r0:r1]
 
-    `src` / `out` are C-contiguous host arrays (n, H, W) / (n, H', W'),
-    page-locked in place for the duration.  ``poison`` (tests): fill the device
+    `src` / `out` are C-contiguous host arrays (n, H, W) / (n, H', W'), moved
+    through the page-locked staging buffers.  ``poison`` (tests): fill the device
     source with NaN bytes first, so a kernel that read a row outside its band's
     [j0, j1) would not match the resident result."""
     t = torch()
@@ -252,32 +330,29 @@ def band_pipeline(src: np.ndarray, dsrc, out: np.ndarray, bands, src_rows, launc
     s_in, s_k, s_out = (t.cuda.Stream(device) for _ in range(3))
     for s in (s_in, s_k, s_out):
         s.wait_stream(cur)
-    rows = _SourceRows(src, dsrc, s_in)
-    row_dst = wd * out_dtype.itemsize
-    freed: list = [None, None]
-    with HostPin(src), HostPin(out):
-        try:
-            for b, ((r0, r1), (j0, j1)) in enumerate(zip(bands, src_rows)):
-                rows.need(j0, j1)
-                ev_in = t.cuda.Event()
-                ev_in.record(s_in)
-                s_k.wait_event(ev_in)
-                if freed[b % 2] is not None:   # the copy-out of band b-2 has drained
-                    s_k.wait_event(freed[b % 2])
-                buf = bufs[b % 2][:, :r1 - r0]
-                launch(b, r0, r1, buf, s_k)
-                ev_k = t.cuda.Event()
-                ev_k.record(s_k)
-                s_out.wait_event(ev_k)
-                for s in range(n):
-                    _copy(out[s, r0:r1].ctypes.data, buf[s].data_ptr(), (r1 - r0) * row_dst,
-                          s_out)
-                freed[b % 2] = t.cuda.Event()
-                freed[b % 2].record(s_out)
-        finally:   # never unpin (or free) while a copy may still be in flight
-            s_in.synchronize()
-            s_k.synchronize()
-            s_out.synchronize()
+    st = _staging()
+    rows = _SourceRows(src, dsrc, s_in, st)
+    prev = None   # the band whose copy-out is pending: it overlaps the next kernel
+    try:
+        for b, ((r0, r1), (j0, j1)) in enumerate(zip(bands, src_rows)):
+            rows.need(j0, j1)
+            ev_in = t.cuda.Event()
+            ev_in.record(s_in)
+            s_k.wait_event(ev_in)
+            buf = bufs[b % 2][:, :r1 - r0]   # band b - 2's copy-out has landed
+            launch(b, r0, r1, buf, s_k)
+            ev_k = t.cuda.Event()
+            ev_k.record(s_k)
+            if prev is not None:
+                _copy_out(st, out, prev, s_out)
+            prev = (r0, r1, buf, ev_k)
+        if prev is not None:
+            _copy_out(st, out, prev, s_out)
+    finally:   # nothing may still use the device buffers when they are freed
+        st.drain()
+        s_in.synchronize()
+        s_k.synchronize()
+        s_out.synchronize()
     return out
 
 
