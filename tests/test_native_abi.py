@@ -92,3 +92,26 @@ def test_argument_errors_are_reported_before_any_device_work():
                                 fake, fake, fake, 4, 4, 1.0, 1.0, 0, 0.0, fake, None)
     assert rc == _native.XRS_ERR_ARG
     assert b"pipeline" in lib.xrs_last_error()
+
+
+def test_library_override_limited_to_probe_arms(tmp_path):
+    """XRS_LIBRARY (A/B timing scripts) may name the product library or an arm
+    under probe/; any other path is refused, so the environment cannot put a
+    different binary behind the product API."""
+    import os
+    import subprocess
+    import sys
+
+    code = ("import xcube_resampling_amd._native as N\n"
+            "try:\n    N.load_library()\n    print('loaded', N.LIB_PATH)\n"
+            "except N.NativeLibraryError as e:\n    print('refused', e)\n")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    fake = tmp_path / "libxrs.so"
+    fake.write_bytes(b"")
+    for value, expect in ((str(fake), "refused"),
+                          (os.path.join(root, "xcube-resampling_amd", "lib", "libxrs.so"),
+                           "loaded")):
+        env = dict(os.environ, XRS_LIBRARY=value)
+        out = subprocess.run([sys.executable, "-c", code], env=env, cwd=root,
+                             capture_output=True, text=True, timeout=120).stdout
+        assert out.startswith(expect), out

@@ -338,8 +338,9 @@ def test_fused_resolve_sampling_equals_k5_then_k6(dtype, interp, n, keep_ij):
 
 
 def test_rectify_dataset_fused_first_variable():
-    """rectify_dataset samples its first device variable inside K5: one and
-    two variables give the same values as each variable rectified alone."""
+    """rectify_dataset samples its first nearest-neighbour device variable
+    inside K5: one and two variables, nearest, bilinear and mixed, give the
+    same values as each variable rectified alone."""
     import xcube_resampling_amd as xrs
 
     rng = np.random.default_rng(3)
@@ -354,14 +355,15 @@ def test_rectify_dataset_fused_first_variable():
                                   "b": xrs.DataArray(b, ("t", "y", "x"))}, coords=coords)
     only_a = xrs.Dataset(data_vars={"a": xrs.DataArray(a, ("y", "x"))}, coords=coords)
     only_b = xrs.Dataset(data_vars={"b": xrs.DataArray(b, ("t", "y", "x"))}, coords=coords)
-    kw = dict(interp_methods="bilinear", tile_size=32)
-    r2 = xrs.rectify_dataset(both, **kw)
-    ra = xrs.rectify_dataset(only_a, **kw)
-    rb = xrs.rectify_dataset(only_b, **kw)
-    assert_bitwise_equal(np.asarray(r2["a"].values), np.asarray(ra["a"].values), "a")
-    assert_bitwise_equal(np.asarray(r2["b"].values), np.asarray(rb["b"].values), "b")
-    assert isinstance(r2["a"].values, np.ndarray) and r2["b"].dims[0] == "t"
-    assert np.isfinite(r2["a"].values).mean() > 0.5
+    for interp in ("nearest", "bilinear", {"a": "nearest", "b": "bilinear"}):
+        kw = dict(interp_methods=interp, tile_size=32)
+        r2 = xrs.rectify_dataset(both, **kw)
+        ra = xrs.rectify_dataset(only_a, **kw)
+        rb = xrs.rectify_dataset(only_b, **kw)
+        assert_bitwise_equal(np.asarray(r2["a"].values), np.asarray(ra["a"].values), f"a {interp}")
+        assert_bitwise_equal(np.asarray(r2["b"].values), np.asarray(rb["b"].values), f"b {interp}")
+        assert isinstance(r2["a"].values, np.ndarray) and r2["b"].dims[0] == "t"
+        assert np.isfinite(r2["a"].values).mean() > 0.5
 
 
 def test_claim_fast_decisions_equal_exact_divisions():

@@ -19,7 +19,27 @@ import threading
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("XRS_LIBRARY", os.path.join(_HERE, "lib", "libxrs.so"))
+PRODUCT_LIB = os.path.join(_HERE, "lib", "libxrs.so")
+PROBE_DIR = os.path.join(os.path.dirname(_HERE), "probe")
+
+
+def _library_path() -> str:
+    """The product library, or — for A/B timing scripts only — an arm built
+    under the repository's probe/ directory named by XRS_LIBRARY (any other
+    path is refused: the environment cannot substitute a product binary)."""
+    path = os.environ.get("XRS_LIBRARY")
+    if not path:
+        return PRODUCT_LIB
+    real = os.path.realpath(path)
+    if real == os.path.realpath(PRODUCT_LIB) or \
+            real.startswith(os.path.realpath(PROBE_DIR) + os.sep):
+        return real
+    raise NativeLibraryError(
+        f"XRS_LIBRARY={path!r}: only the product library or an A/B arm under "
+        f"{PROBE_DIR} may be loaded")
+
+
+_LIB_PATH_ERROR = None
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "xrs.h")
 
 XRS_OK = 0
@@ -50,6 +70,12 @@ DTYPE_CODES = {
 
 class NativeLibraryError(RuntimeError):
     """libxrs.so could not be loaded or a HIP call failed."""
+
+
+try:   # the library this process loads (XRS_LIBRARY: probe arms only)
+    LIB_PATH = _library_path()
+except NativeLibraryError as _e:
+    LIB_PATH, _LIB_PATH_ERROR = None, _e
 
 
 _c_i64 = ctypes.c_int64
@@ -178,8 +204,12 @@ def declared_symbols(header: str = HEADER_PATH) -> list[str]:
     return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\**\s+\**(xrs_\w+)\s*\(", text, re.M)))
 
 
-def load_library(path: str = LIB_PATH):
+def load_library(path: str | None = None):
     """Load libxrs.so without requiring a GPU (symbol checks, CPU tests)."""
+    if path is None:
+        if LIB_PATH is None:
+            raise _LIB_PATH_ERROR
+        path = LIB_PATH
     if not os.path.exists(path):
         raise NativeLibraryError(
             f"libxrs.so not found at {path}: build it with "
