@@ -263,16 +263,27 @@ def device_copy_rate(lib, src, stream, warm: int = 40, timed: int = 20) -> float
     return 2 * nbytes / (ms / 1e3) / 1e9
 
 
-def shader_clock_ghz(lib, stream, blocks: int = 1024, spin: int = 3000) -> float:
-    """Median over blocks of d(s_memtime) / d(s_memrealtime) x 100 MHz."""
+def clock_probe_launch(lib, stream, blocks: int = 1024, spin: int = 3000):
+    """Queue the shader-clock probe on `stream` (no host wait: the GPU stays
+    busy); clock_probe_read() takes its result later."""
     import torch
 
     buf = torch.zeros((blocks, 2), dtype=torch.int64, device=stream.device)
     if lib.xrs_bench_clock_probe(buf.data_ptr(), blocks, spin, int(stream.cuda_stream)) != 0:
         raise RuntimeError("benchlib clock probe failed")
-    stream.synchronize()
+    return buf
+
+
+def clock_probe_read(buf) -> float:
+    """Median over blocks of d(s_memtime) / d(s_memrealtime) x 100 MHz."""
     d = buf.cpu().numpy()
     return round(float(np.median(d[:, 0] / np.maximum(d[:, 1], 1))) * 0.1, 3)
+
+
+def shader_clock_ghz(lib, stream, blocks: int = 1024, spin: int = 3000) -> float:
+    buf = clock_probe_launch(lib, stream, blocks, spin)
+    stream.synchronize()
+    return clock_probe_read(buf)
 
 
 def main():
@@ -373,17 +384,21 @@ def main():
             with torch.cuda.graph(g):
                 step()
             run = g.replay
+        barrier()   # the first collective sets the communicator up: not between warm-up and timing
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         # the same-run device-copy rate, measured back to back with the warm-up
         # steps: its ~0.1 s of streaming also takes the shader clock to its
         # loaded level (DVFS: ~30 ms of load from idle), as W steps alone may not
         copy_rates.append(device_copy_rate(benchlib, src, stream))
         for _ in range(warmup):
             run()
-        torch.cuda.synchronize()
-        clk0 = shader_clock_ghz(benchlib, stream)   # outside the timed region
+        # nothing on the host between the warm-up and the timed steps but the
+        # barrier and the synchronize: an idle gap of a few ms lets the clock
+        # drop, and the first timed launches ramp up again (kernel trace of
+        # r03's first version: 17.6 ms of host work here, then 3.0 -> 2.5 ms)
+        probe0 = clock_probe_launch(benchlib, stream)   # read after the timed steps
         barrier()
         torch.cuda.synchronize()
-        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
         ev0.record(stream)
         for _ in range(steps):
@@ -392,6 +407,7 @@ def main():
         torch.cuda.synchronize()
         barrier()
         t1 = time.perf_counter()
+        clk0 = clock_probe_read(probe0)
         clk1 = shader_clock_ghz(benchlib, stream)
         wall = max_over_ranks(t1 - t0, device) / steps * 1e3
         return wall, ev0.elapsed_time(ev1) / steps, (clk0, clk1)

@@ -8,5 +8,7 @@ bash scripts/gpu_round.sh $OUT; rc=$?
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 timeout -k 10 600 python -u scripts/bench_configs.py --configs 1,2,2u,3,4 --cpu-seconds 8 > $OUT/configs.jsonl 2> $OUT/configs.err || exit $?
 cut -c1-160 $OUT/configs.jsonl
-bash scripts/gpu_rect_probes.sh $OUT/rect || exit $?
+timeout -k 10 300 python -u bench.py --warmup 5 --steps 20 > $OUT/bench_w5.json 2> $OUT/bench_w5.err || exit $?
+cut -c1-300 $OUT/bench_w5.json
+bash scripts/gpu_rect3.sh $OUT/rect fused || exit $?
 exit $rc
