@@ -5,7 +5,7 @@ host RAM -> numpy result, bilinear EPSG:4326 -> EPSG:3857 (config 5 geometry).
 
   whole     : torch copy of the whole raster to HBM, one K1 launch, copy back
               (what a direct port of the reference's numpy path does)
-  streamed  : streaming.reproject_host — arrays page-locked in place, target
+  streamed  : streaming.reproject_host — through page-locked staging buffers, target
               bands of 2048 rows, H2D / K1 / D2H on three streams
 
 One JSON line per mode: wall seconds (best of reps) and Mpixels/s, i.e. the
