@@ -71,6 +71,35 @@ def test_device_transform_matches_numpy_restatement(src, dst):
     np.testing.assert_array_equal(iy, dy)
 
 
+@pytest.mark.parametrize("lat_0,lon_0,dst", [(0.0, 9.0, "EPSG:32632"),      # equatorial aspect
+                                              (90.0, 0.0, "EPSG:32633"),     # polar (generic)
+                                              (52.0, 10.0, "EPSG:32632")])   # oblique, not 3035
+def test_laea_aspects_to_utm_match_numpy(lat_0, lon_0, dst):
+    """LAEA -> UTM through the sine/cosine pipeline (equatorial and oblique
+    aspects, proj::laea_inv_tmerc_fwd) and the two-step one (polar aspect):
+    the numpy restatement to a few ulps, non-finite in the same places."""
+    import xcube_resampling_amd as xrs
+    from xcube_resampling_amd import kernels
+
+    laea = xrs.CRS.from_cf({"grid_mapping_name": "lambert_azimuthal_equal_area",
+                            "latitude_of_projection_origin": lat_0,
+                            "longitude_of_projection_origin": lon_0,
+                            "false_easting": 1.0e6, "false_northing": 5.0e5,
+                            "inverse_flattening": 298.257223563})
+    tr = xrs.Transformer.from_crs(laea, dst, always_xy=True)
+    gx, gy = np.linspace(-4.0e6, 6.0e6, 241), np.linspace(-5.0e6, 5.0e6, 257)
+    gy = np.concatenate([gy, [5.0e5]])   # the projection centre row
+    gx = np.concatenate([gx, [1.0e6]])
+    xx, yy = np.meshgrid(gx, gy)
+    ex, ey = tr.transform(xx, yy)
+    dx, dy = (t.cpu().numpy() for t in kernels.transform(tr, gx, gy, True))
+    for got, exp in ((dx, ex), (dy, ey)):
+        fin = np.isfinite(exp)
+        np.testing.assert_array_equal(np.isfinite(got), fin)
+        assert fin.sum() > 0.2 * fin.size
+        np.testing.assert_allclose(got[fin], exp[fin], rtol=RTOL, atol=ATOL["m"])
+
+
 def test_device_transform_nan_inputs():
     import xcube_resampling_amd as xrs
     from xcube_resampling_amd import kernels
