@@ -397,7 +397,8 @@ def main():
         # drop, and the first timed launches ramp up again (kernel trace of
         # r03's first version: 17.6 ms of host work here, then 3.0 -> 2.5 ms)
         probe0 = clock_probe_launch(benchlib, stream)   # read after the timed steps
-        barrier()
+        torch.cuda.synchronize()   # every rank's own queue drained ...
+        barrier()                  # ... before the ranks start together
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         ev0.record(stream)
