@@ -212,3 +212,29 @@ def test_rectify_streamed_matches_resident(band_rows, reverse):
         out = streaming.rectify_host(src, ij, interp, np.nan, band_rows=band_rows, poison=True)
         assert_bitwise_equal(out, ref, f"rectify {interp} band_rows={band_rows}")
     assert np.isfinite(ref).mean() > 0.4
+
+
+def test_staging_round_trip_multi_chunk():
+    """host_to_device / device_to_host through the staging buffers: arrays of
+    several 16 MiB chunks plus a ragged tail, odd dtypes and a read-only view,
+    land bit for bit; the pinned buffers are reused across calls."""
+    from xcube_resampling_amd import streaming
+    from xcube_resampling_amd.options import set_options
+
+    rng = np.random.default_rng(9)
+    n = 3 * (streaming._STAGE_BYTES // 4) + 12345
+    cases = [rng.random(n, dtype=np.float32).reshape(-1, 5) if n % 5 == 0 else
+             rng.random(n, dtype=np.float32),
+             rng.integers(-2**15, 2**15, 2 * streaming._STAGE_BYTES // 2 + 7, dtype=np.int16),
+             rng.random((1000, 2049))]
+    ro = rng.random((3000, 3001))
+    ro.flags.writeable = False
+    cases.append(ro)
+    with set_options(host_streaming_min_bytes=0):
+        for a in cases:
+            d = streaming.host_to_device(a, "cuda:0")
+            assert tuple(d.shape) == a.shape
+            back = streaming.device_to_host(d)
+            assert back.dtype == a.dtype
+            assert np.array_equal(back.view(np.uint8), np.ascontiguousarray(a).view(np.uint8))
+    assert streaming._STAGING is not None and len(streaming._STAGING.bufs) == 2
