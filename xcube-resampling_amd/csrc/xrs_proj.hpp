@@ -20,6 +20,59 @@ namespace proj {
 constexpr double kDegToRad = 0.017453292519943296;   // crs._DEG_TO_RAD
 constexpr double kPi = 3.141592653589793;
 
+// ---- f64 log / atan2 for the projection pipelines ---------------------------------
+// The classic fdlibm reductions and minimax coefficients (e_log.c, s_atan.c;
+// within 1 ulp of the correctly rounded result, 2 ulp for atan2 through the
+// pi - r fold), written without branches: the library's versions are ~1.6x
+// longer and the transform is VALU-issue bound.
+// log(x) for x >= 1 (NaN and +inf pass through).
+__device__ inline double log_ge1(double x) {
+  constexpr double kLg1 = 6.666666666666735130e-01, kLg2 = 3.999999999940941908e-01,
+                   kLg3 = 2.857142874366239149e-01, kLg4 = 2.222219843214978396e-01,
+                   kLg5 = 1.818357216161805012e-01, kLg6 = 1.531383769920937332e-01,
+                   kLg7 = 1.479819860511658591e-01;
+  constexpr double kLn2Hi = 6.93147180369123816490e-01, kLn2Lo = 1.90821492927058770002e-10;
+  int e;
+  double m = frexp(x, &e);                  // x = m 2^e, m in [0.5, 1)
+  const bool lo = m < 0.70710678118654752440;
+  m = lo ? m + m : m;                       // m in [sqrt(1/2), sqrt(2))
+  const double dk = (double)(lo ? e - 1 : e);
+  const double f = m - 1.0;
+  const double sv = f / (2.0 + f), z = sv * sv, w = z * z;
+  const double t1 = w * (kLg2 + w * (kLg4 + w * kLg6));
+  const double t2 = z * (kLg1 + w * (kLg3 + w * (kLg5 + w * kLg7)));
+  const double hfsq = 0.5 * f * f;
+  const double r = dk * kLn2Hi - ((hfsq - (sv * (hfsq + t2 + t1) + dk * kLn2Lo)) - f);
+  return x < INFINITY ? r : x;
+}
+
+// atan2(y, x) (not for both arguments 0 or infinite: the pipelines turn
+// such points into non-finite results anyway)
+__device__ inline double atan2_pp(double y, double x) {
+  constexpr double kAt[11] = {3.33333333333329318027e-01, -1.99999999998764832476e-01,
+                              1.42857142725034663711e-01, -1.11111104054623557880e-01,
+                              9.09088713343650656196e-02, -7.69187620504482999495e-02,
+                              6.66107313738753120669e-02, -5.83357013379057348645e-02,
+                              4.97687799461593236017e-02, -3.65315727442169155270e-02,
+                              1.62858201153657823623e-02};
+  const double ax = fabs(x), ay = fabs(y);
+  const bool swap = ay > ax;
+  const double a = (swap ? ax : ay) / (swap ? ay : ax);       // in [0, 1]
+  const bool r0 = a >= 0.4375, r1 = a >= 0.6875;              // atan(1/2), atan(1) bands
+  const double num = r1 ? a - 1.0 : (r0 ? 2.0 * a - 1.0 : a);
+  const double den = r1 ? a + 1.0 : (r0 ? 2.0 + a : 1.0);
+  const double t = num / den, z = t * t, w = z * z;
+  const double s1 =
+      z * (kAt[0] + w * (kAt[2] + w * (kAt[4] + w * (kAt[6] + w * (kAt[8] + w * kAt[10])))));
+  const double s2 = w * (kAt[1] + w * (kAt[3] + w * (kAt[5] + w * (kAt[7] + w * kAt[9]))));
+  const double hi = r1 ? 7.85398163397448278999e-01 : 4.63647609000806093515e-01;
+  const double lo = r1 ? 3.06161699786838301793e-17 : 2.26987774529616870924e-17;
+  double r = r0 ? hi - ((t * (s1 + s2) - lo) - t) : t - t * (s1 + s2);
+  r = swap ? 1.57079632679489655800e+00 - (r - 6.12323399573676603587e-17) : r;
+  r = x < 0.0 ? 3.1415926535897931160e+00 - (r - 1.2246467991473531772e-16) : r;
+  return copysign(r, y);
+}
+
 // ---- PROJ helpers (projections.py) ---------------------------------------------
 // Clenshaw summation for the Gaussian <-> geodetic latitude (tmerc.cpp gatg)
 __device__ inline double gatg(const double* p, double B, double cos_2B, double sin_2B) {
@@ -60,7 +113,7 @@ __device__ inline void tmerc_fwd_tail(const XrsProjStep& s, double sin_Cn, doubl
                                       double sin_Ce, double cos_Ce, double& x, double& y) {
   const double* gtu = s.c + 18;
   const double cos_Cn_cos_Ce = cos_Cn * cos_Ce;
-  double Cn = atan2(sin_Cn, cos_Cn_cos_Ce);
+  double Cn = atan2_pp(sin_Cn, cos_Cn_cos_Ce);
   // |(sin_Cn, cos_Cn cos_Ce)| <= 1: no scaling needed; rsqrt (within an ulp)
   // instead of hypot's scaled sequence and a division
   const double inv_denom_tan_Ce = rsqrt(sin_Cn * sin_Cn + cos_Cn_cos_Ce * cos_Cn_cos_Ce);
@@ -68,7 +121,7 @@ __device__ inline void tmerc_fwd_tail(const XrsProjStep& s, double sin_Cn, doubl
   // asinh through log (|tan_Ce| < 7 here: no overflow guard needed; absolute
   // error ~1e-16, i.e. ~1e-9 m, where the library's asinh keeps relative
   // precision near 0 at 1.6x the instructions)
-  double Ce = copysign(log(fabs(tan_Ce) + sqrt(tan_Ce * tan_Ce + 1.0)), tan_Ce);
+  double Ce = copysign(log_ge1(fabs(tan_Ce) + sqrt(tan_Ce * tan_Ce + 1.0)), tan_Ce);
   const double two_inv_denom_tan_Ce = 2 * inv_denom_tan_Ce;
   const double two_inv_denom_tan_Ce_square = two_inv_denom_tan_Ce * inv_denom_tan_Ce;
   const double tmp_r = cos_Cn_cos_Ce * two_inv_denom_tan_Ce_square;

@@ -320,6 +320,15 @@ def reproject_dataset(source_ds, target_gm: GridMapping, source_gm: GridMapping 
         source_ds, source_gm, target_gm, transformer, interp_methods, agg_methods, recover_nans)
 
     plan = plan_reproject(source_gm, target_gm, transformer)
+    yx_dims = (source_gm.xy_dim_names[1], source_gm.xy_dim_names[0])
+    n_vars = sum(1 for v in source_ds.data_vars.values() if v.dims[-2:] == yx_dims)
+    if n_vars == 1 and plan.coord_mode == 1 and plan.src_x is None:
+        # one variable over a non-separable pair: the transformation fused into
+        # the gather (xrs_reproject_proj) beats tables made for one reader
+        # (config 2u: 1.58 vs 1.63 ms of kernels; bit-identical results)
+        import dataclasses
+
+        plan = dataclasses.replace(plan, fuse_transform=True)
 
     x_name, y_name = source_gm.xy_var_names
     coords = {k: v for k, v in source_ds.coords.items() if k not in (x_name, y_name)}
@@ -329,7 +338,6 @@ def reproject_dataset(source_ds, target_gm: GridMapping, source_gm: GridMapping 
     coords["spatial_ref"] = DataArray(np.array(0), (), target_gm.crs.to_cf())
     target_ds = Dataset(coords=coords, attrs=source_ds.attrs)
 
-    yx_dims = (source_gm.xy_dim_names[1], source_gm.xy_dim_names[0])
     for var_name, data_array in source_ds.items():
         if data_array.dims[-2:] == yx_dims:
             assert len(data_array.dims) in (2, 3), \
