@@ -250,9 +250,12 @@ def test_streamed_host_source_fuses_when_tables_exceed_budget():
     sgm = xrs.GridMapping.from_coords(xrs.DataArray(x, "x", name="x"),
                                       xrs.DataArray(y, "y", name="y"), "EPSG:32632")
 
-    def run():
-        ds = xrs.Dataset(data_vars={"v": (("t", "y", "x"), a)},
-                         coords={"x": ("x", x), "y": ("y", y)})
+    def run(one_var=False):
+        # two variables: the tables are the default (one variable fuses, below)
+        dv = {"v": (("t", "y", "x"), a)}
+        if not one_var:
+            dv["w"] = (("t", "y", "x"), a[::-1].copy())
+        ds = xrs.Dataset(data_vars=dv, coords={"x": ("x", x), "y": ("y", y)})
         with xrs.set_options(host_streaming_min_bytes=0):
             return xrs.reproject_dataset(ds, tgm, source_gm=sgm, interp_methods="bilinear")["v"]
 
@@ -270,11 +273,15 @@ def test_streamed_host_source_fuses_when_tables_exceed_budget():
         with xrs.set_options(reproject_table_max_bytes=0):
             got = run().values
         assert calls   # every band through xrs_reproject_proj
+        calls.clear()
+        one = run(one_var=True).values   # one variable: fused by default
+        assert calls
     finally:
         kernels._reproject_proj = orig
     assert isinstance(ref, np.ndarray) and isinstance(got, np.ndarray)   # host in, host out
     assert np.isfinite(ref).mean() > 0.5
     assert np.array_equal(ref, got, equal_nan=True)
+    assert np.array_equal(ref, one, equal_nan=True)
     torch.cuda.synchronize()
 
 
