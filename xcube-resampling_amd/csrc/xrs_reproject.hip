@@ -472,6 +472,10 @@ gather_2d_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t bands_per_til
 }
 
 // ---- K1p: per-pixel gather with the projection fused (non-separable pairs) --
+constexpr int kModeAny = -1;
+constexpr int kModeF32Nearest = XRS_DTYPE_F32 * 4 + 0;
+constexpr int kModeF32BilinearF64 = XRS_DTYPE_F32 * 4 + 3;
+constexpr int kModeF64BilinearF64 = XRS_DTYPE_F64 * 4 + 3;
 // reproject.py:472-496 + 268-335 for one target pixel: its centre
 // (grid_x[c], grid_y[r]) goes through the pipeline (xrs_proj.hpp, the code
 // xrs_transform runs), then the index math and the taps of every dim-0 slice.
@@ -505,42 +509,100 @@ __device__ inline void gather_pixel_any(int mode, const GatherArgs& a, int64_t r
   }
 }
 
-template <int K0, int K1, int FAST>
+// one (dtype, variant) as a template: the hot modes get kernels of their own
+// (the switch keeps every case's arguments live, and those SGPRs spilled into
+// VGPR lanes and were read back inside the projection)
+template <int MODE>
+__device__ inline void gather_pixel_mode(const GatherArgs& a, int64_t r, int64_t col,
+                                         const AxisEntry& ex, const AxisEntry& ey) {
+  if constexpr (MODE == kModeF32Nearest)
+    gather_pixel<float, float, XRS_INTERP_NEAREST>(a, r, col, ex, ey);
+  else if constexpr (MODE == kModeF32BilinearF64)
+    gather_pixel<float, double, XRS_INTERP_BILINEAR>(a, r, col, ex, ey);
+  else if constexpr (MODE == kModeF64BilinearF64)
+    gather_pixel<double, double, XRS_INTERP_BILINEAR>(a, r, col, ex, ey);
+}
+
+// n / d for n < 2^31 by a multiply-high (the round-up method: m = floor(2^32
+// (2^l - d) / d) + 1, l = ceil(log2 d); exact for every such n and d >= 1)
+struct DivU32 {
+  uint32_t m, l;
+  static DivU32 make(uint32_t d) {
+    uint32_t l = 0;
+    while ((1ull << l) < d) ++l;
+    return DivU32{(uint32_t)((((1ull << l) - d) << 32) / d + 1), l};
+  }
+  __device__ uint32_t div(uint32_t n) const { return (__umulhi(n, m) + n) >> l; }
+};
+
+// The gather's arguments read again from the kernel-argument segment (scalar
+// loads; the kernel's first argument sits at offset 0), after `dep` — the
+// pixel's projection — is computed.  The asm makes the segment address opaque
+// per iteration, so the loads stay next to their uses: kept live across the
+// loop instead, they and the projection's constants outnumbered the SGPRs, and
+// the spilled ones were read back from VGPR lanes (v_readlane, ~110 VALU
+// instructions per pixel) inside the projection.
+__device__ inline GatherArgs gather_args_after(double dep) {
+#if __HIP_DEVICE_COMPILE__   // (the host pass only parses device functions)
+  typedef const __attribute__((address_space(4))) GatherArgs* ArgsPtr;
+  uint64_t kp = reinterpret_cast<uint64_t>(__builtin_amdgcn_kernarg_segment_ptr());
+  asm volatile("" : "+s"(kp) : "v"(dep));
+  return *reinterpret_cast<ArgsPtr>(kp);
+#else
+  return GatherArgs{};
+#endif
+}
+
+template <int K0, int K1, int FAST, int MODE>
 __global__ void __launch_bounds__(kThreads)
-gather_proj_kernel(GatherArgs a, XrsProjStep s0, XrsProjStep s1, int mode) {
+gather_proj_kernel(GatherArgs a, XrsProjStep s0, XrsProjStep s1, int mode, DivU32 div_th,
+                   DivU32 div_tw) {
   const proj::Pipeline<K0, K1, FAST> pipe(s0, s1);
   // one target pixel per thread and step, grid-stride over the rows of the
   // launch (lanes on consecutive columns): the loop carries almost no state
   // beside the projection's registers (a tile-item loop cost it one wave per
   // SIMD of occupancy)
   const Geometry& g = a.g;
-  const bool nearest = (mode & 3) == 0;
-  const uint32_t w32 = (uint32_t)g.dst_w, th = (uint32_t)g.tile_h, tw = (uint32_t)g.tile_w;
-  const uint32_t ntx = (uint32_t)g.ntiles_x;
-  const int64_t p0 = g.row_begin * g.dst_w, np = (g.row_end - g.row_begin) * g.dst_w;
+  const bool nearest = MODE >= 0 ? (MODE & 3) == 0 : (mode & 3) == 0;
+  const uint32_t w32 = (uint32_t)g.dst_w;
+  const int64_t np = (g.row_end - g.row_begin) * g.dst_w;
+  // the pixel's row and column step by (S / W, S % W) per grid stride S (no
+  // 64-bit division per pixel); rows and columns are < 2^31 (checked at launch)
+  const int64_t q0 = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  const int64_t S = (int64_t)gridDim.x * kThreads;
+  const uint32_t sr = (uint32_t)(S / g.dst_w), sc = (uint32_t)(S - (int64_t)sr * g.dst_w);
+  uint32_t r = (uint32_t)(g.row_begin + q0 / g.dst_w), c = (uint32_t)(q0 % g.dst_w);
   int32_t eflags = 0;
-  for (int64_t q = (int64_t)blockIdx.x * kThreads + threadIdx.x; q < np;
-       q += (int64_t)gridDim.x * kThreads) {
-    const int64_t p = p0 + q;
-    const uint32_t r = (uint32_t)(p / g.dst_w), c = (uint32_t)(p - (int64_t)r * w32);
-    const uint32_t t = (r / th) * ntx + c / tw;
+  for (int64_t q = q0; q < np; q += S) {
     double px = g.src_x[c], py = g.src_y[r];   // the target pixel centre
     pipe(s0, s1, px, py);
-    const float x0 = g.tile_x0[t], y0 = g.tile_y0[t];
-    const int64_t wi0 = g.tile_win[2 * t], wj0 = g.tile_win[2 * t + 1];
+    const GatherArgs ga = gather_args_after(px);
+    const Geometry& gg = ga.g;
+    const uint32_t t = div_th.div(r) * (uint32_t)gg.ntiles_x + div_tw.div(c);
+    const float x0 = gg.tile_x0[t], y0 = gg.tile_y0[t];
+    const int64_t wi0 = gg.tile_win[2 * t], wj0 = gg.tile_win[2 * t + 1];
     AxisEntry ex, ey;
     if (nearest) {
-      ex = resolve_axis<XRS_INTERP_NEAREST>(px, x0, g.x_res, g.win_w, wi0, g.src_w, 0, g.src_w,
+      ex = resolve_axis<XRS_INTERP_NEAREST>(px, x0, gg.x_res, gg.win_w, wi0, gg.src_w, 0, gg.src_w,
                                             eflags);
-      ey = resolve_axis<XRS_INTERP_NEAREST>(py, y0, g.neg_y_res, g.win_h, wj0, g.src_h,
-                                            g.src_row0, g.src_rows, eflags);
+      ey = resolve_axis<XRS_INTERP_NEAREST>(py, y0, gg.neg_y_res, gg.win_h, wj0, gg.src_h,
+                                            gg.src_row0, gg.src_rows, eflags);
     } else {
-      ex = resolve_axis<XRS_INTERP_BILINEAR>(px, x0, g.x_res, g.win_w, wi0, g.src_w, 0, g.src_w,
+      ex = resolve_axis<XRS_INTERP_BILINEAR>(px, x0, gg.x_res, gg.win_w, wi0, gg.src_w, 0, gg.src_w,
                                              eflags);
-      ey = resolve_axis<XRS_INTERP_BILINEAR>(py, y0, g.neg_y_res, g.win_h, wj0, g.src_h,
-                                             g.src_row0, g.src_rows, eflags);
+      ey = resolve_axis<XRS_INTERP_BILINEAR>(py, y0, gg.neg_y_res, gg.win_h, wj0, gg.src_h,
+                                             gg.src_row0, gg.src_rows, eflags);
     }
-    gather_pixel_any(mode, a, r, c, ex, ey);
+    if constexpr (MODE >= 0)
+      gather_pixel_mode<MODE>(ga, r, c, ex, ey);
+    else
+      gather_pixel_any(mode, ga, r, c, ex, ey);
+    c += sc;
+    r += sr;
+    if (c >= w32) {
+      c -= w32;
+      ++r;
+    }
   }
   if (eflags) atomicOr(g.err_flags, eflags);
 }
@@ -601,6 +663,26 @@ int launch(const GatherArgs& a, int coord_mode, AxisEntry* xtab, AxisEntry* ytab
   return XRS_OK;
 }
 
+template <int K0, int K1, int FAST>
+void launch_proj_mode(int nb, const GatherArgs& a, const XrsProjStep& s0, const XrsProjStep& s1,
+                      int mode, hipStream_t stream) {
+  const DivU32 dh = DivU32::make((uint32_t)a.g.tile_h), dw = DivU32::make((uint32_t)a.g.tile_w);
+  switch (mode) {
+#define XRS_KP(M)                                                                          \
+  case M:                                                                                  \
+    hipLaunchKernelGGL((gather_proj_kernel<K0, K1, FAST, M>), dim3(nb), dim3(kThreads), 0, \
+                       stream, a, s0, s1, mode, dh, dw);                                   \
+    break;
+    XRS_KP(kModeF32Nearest)
+    XRS_KP(kModeF32BilinearF64)
+    XRS_KP(kModeF64BilinearF64)
+#undef XRS_KP
+    default:
+      hipLaunchKernelGGL((gather_proj_kernel<K0, K1, FAST, kModeAny>), dim3(nb), dim3(kThreads),
+                         0, stream, a, s0, s1, mode, dh, dw);
+  }
+}
+
 template <int K0, int K1>
 int launch_proj(const GatherArgs& a, const XrsProjStep& s0, const XrsProjStep& s1, int mode,
                 hipStream_t stream) {
@@ -611,14 +693,11 @@ int launch_proj(const GatherArgs& a, const XrsProjStep& s0, const XrsProjStep& s
   if constexpr (K0 == XRS_PROJ_LAEA_INV && K1 == XRS_PROJ_TMERC_FWD)
     fast = proj::fast_kind(K0, K1, s0);
   if (fast == proj::kFastObliq)
-    hipLaunchKernelGGL((gather_proj_kernel<K0, K1, proj::kFastObliq>), dim3(nb), dim3(kThreads),
-                       0, stream, a, s0, s1, mode);
+    launch_proj_mode<K0, K1, proj::kFastObliq>(nb, a, s0, s1, mode, stream);
   else if (fast == proj::kFastEquit)
-    hipLaunchKernelGGL((gather_proj_kernel<K0, K1, proj::kFastEquit>), dim3(nb), dim3(kThreads),
-                       0, stream, a, s0, s1, mode);
+    launch_proj_mode<K0, K1, proj::kFastEquit>(nb, a, s0, s1, mode, stream);
   else
-    hipLaunchKernelGGL((gather_proj_kernel<K0, K1, proj::kFastNone>), dim3(nb), dim3(kThreads),
-                       0, stream, a, s0, s1, mode);
+    launch_proj_mode<K0, K1, proj::kFastNone>(nb, a, s0, s1, mode, stream);
   XRS_HIP_CHECK(hipGetLastError());
   return XRS_OK;
 }
