@@ -223,6 +223,25 @@ inline int resident_blocks(const void* kernel, int threads, size_t dyn_lds = 0) 
   return (per_cu > 0 ? per_cu : 1) * (cus > 0 ? cus : 1);
 }
 
+// A kernel argument (an arguments struct at byte OFFSET of the kernel-argument
+// segment: 0 for the first argument) read again, after `dep` is computed.
+// The asm makes the segment address opaque at this point, so the scalar loads
+// stay next to their uses: large argument structs kept live across a kernel's
+// loop, together with the loop's own uniform values, outnumber the SGPRs, and
+// the spilled ones are read back from VGPR lanes (v_readlane, one VALU
+// instruction each) on every iteration.
+template <typename A, size_t OFFSET = 0>
+__device__ inline A kernel_arg_after(double dep) {
+#if __HIP_DEVICE_COMPILE__   // (the host pass only parses device functions)
+  typedef const __attribute__((address_space(4))) A* ArgPtr;
+  uint64_t kp = reinterpret_cast<uint64_t>(__builtin_amdgcn_kernarg_segment_ptr()) + OFFSET;
+  asm volatile("" : "+s"(kp) : "v"(dep));
+  return *reinterpret_cast<ArgPtr>(kp);
+#else
+  return A{};
+#endif
+}
+
 }  // namespace xrs
 
 // Thread-local error message reported through xrs_last_error().

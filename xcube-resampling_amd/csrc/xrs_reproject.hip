@@ -427,12 +427,14 @@ gather_2d_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t bands_per_til
                                             g.src_row0, g.src_rows, eflags);
           }
         }
-      const T fill = Conv<T>::from_f64(a.fill);
-      for (int64_t sn = 0; sn < a.n; ++sn) {
-        const T* src = static_cast<const T*>(a.src) + sn * a.src_sn;
-        O* dst = static_cast<O*>(a.dst) + sn * a.dst_sn + (r - g.row_begin) * a.dst_sy + it.c0;
+      // the tap phase's arguments re-read here (kernel_arg_after: SGPR spills)
+      const GatherArgs ga = kernel_arg_after<GatherArgs>(ex[0][0].d);
+      const T fill = Conv<T>::from_f64(ga.fill);
+      for (int64_t sn = 0; sn < ga.n; ++sn) {
+        const T* src = static_cast<const T*>(ga.src) + sn * ga.src_sn;
+        O* dst = static_cast<O*>(ga.dst) + sn * ga.dst_sn + (r - ga.g.row_begin) * ga.dst_sy + it.c0;
         auto at = [&](int32_t row, int32_t c) -> T {
-          return src[(int64_t)max(row, 0) * a.src_sy + max(c, 0)];
+          return src[(int64_t)max(row, 0) * ga.src_sy + max(c, 0)];
         };
         T t[kRows2D][kPx][4];
 #pragma unroll
@@ -463,7 +465,7 @@ gather_2d_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t bands_per_til
               const T v11 = (fy.c >= 0 && fx.c >= 0) ? t[q][k][3] : fill;
               out = Conv<O>::from_f64(interp4<T, INTERP>(v00, v01, v10, v11, fx.d, fy.d));
             }
-            dst[q * a.dst_sy + (int)threadIdx.x + k * kThreads] = out;
+            dst[q * ga.dst_sy + (int)threadIdx.x + k * kThreads] = out;
           }
       }
     }
@@ -535,24 +537,6 @@ struct DivU32 {
   __device__ uint32_t div(uint32_t n) const { return (__umulhi(n, m) + n) >> l; }
 };
 
-// The gather's arguments read again from the kernel-argument segment (scalar
-// loads; the kernel's first argument sits at offset 0), after `dep` — the
-// pixel's projection — is computed.  The asm makes the segment address opaque
-// per iteration, so the loads stay next to their uses: kept live across the
-// loop instead, they and the projection's constants outnumbered the SGPRs, and
-// the spilled ones were read back from VGPR lanes (v_readlane, ~110 VALU
-// instructions per pixel) inside the projection.
-__device__ inline GatherArgs gather_args_after(double dep) {
-#if __HIP_DEVICE_COMPILE__   // (the host pass only parses device functions)
-  typedef const __attribute__((address_space(4))) GatherArgs* ArgsPtr;
-  uint64_t kp = reinterpret_cast<uint64_t>(__builtin_amdgcn_kernarg_segment_ptr());
-  asm volatile("" : "+s"(kp) : "v"(dep));
-  return *reinterpret_cast<ArgsPtr>(kp);
-#else
-  return GatherArgs{};
-#endif
-}
-
 template <int K0, int K1, int FAST, int MODE>
 __global__ void __launch_bounds__(kThreads)
 gather_proj_kernel(GatherArgs a, XrsProjStep s0, XrsProjStep s1, int mode, DivU32 div_th,
@@ -576,7 +560,9 @@ gather_proj_kernel(GatherArgs a, XrsProjStep s0, XrsProjStep s1, int mode, DivU3
   for (int64_t q = q0; q < np; q += S) {
     double px = g.src_x[c], py = g.src_y[r];   // the target pixel centre
     pipe(s0, s1, px, py);
-    const GatherArgs ga = gather_args_after(px);
+    // the gather's arguments re-read after the projection (kernel_arg_after:
+    // kept live through it, they spilled ~110 SGPRs' reads into the projection)
+    const GatherArgs ga = kernel_arg_after<GatherArgs>(px);
     const Geometry& gg = ga.g;
     const uint32_t t = div_th.div(r) * (uint32_t)gg.ntiles_x + div_tw.div(c);
     const float x0 = gg.tile_x0[t], y0 = gg.tile_y0[t];
