@@ -340,7 +340,11 @@ def main():
     dev_index = local_rank % torch.cuda.device_count() if backend == "gloo" else local_rank
     torch.cuda.set_device(dev_index)
     device = torch.device("cuda", dev_index)
-    if world > 1:
+    # XRS_BENCH_DIST=1: the process group and every collective of the N > 1
+    # path also at N = 1 (a one-GPU rehearsal of the RCCL calls the driver's
+    # multi-GPU runs make)
+    use_dist = world > 1 or os.environ.get("XRS_BENCH_DIST") == "1"
+    if use_dist:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=device)
@@ -368,7 +372,7 @@ def main():
         return step
 
     def barrier():
-        if world > 1:
+        if use_dist:
             if backend == "nccl":
                 dist.barrier(device_ids=[dev_index])
             else:
@@ -439,7 +443,7 @@ def main():
         del out64
 
     rank_ms = None
-    if world > 1:   # whole-job bytes, slowest rank's kernel time, every rank's time
+    if use_dist:   # whole-job bytes, slowest rank's kernel time, every rank's time
         t = torch.tensor([float(my_bytes)], dtype=torch.float64,
                          device=device if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
@@ -528,7 +532,7 @@ def main():
         if cpu is not None:
             res["cpu_baseline"] = cpu
         print(json.dumps(res), flush=True)
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
 
 

@@ -683,6 +683,10 @@ rectify_claim_kernel(RectArgs a) {
     const int32_t qi = ti.si0 + pcol;
     const int32_t r0 = cy * kStripH;
     const int32_t r_end = min(r0 + kStripH, nq_j);
+    if (r0 >= r_end) {   // wave-uniform: a strip past the window (inconsistent offsets)
+      if (lane == 0) atomicOr(a.err_flags, XRS_EFLAG_STATE);
+      continue;
+    }
     auto load_pt = [&](int32_t qj) {
       StripPoint p{NAN, NAN};
       if (has_pt) {

@@ -313,7 +313,7 @@ def max_over_ranks(value: float, device=None) -> float:
     import torch
     import torch.distributed as dist
 
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if not (dist.is_available() and dist.is_initialized()):
         return float(value)
     if dist.get_backend() == "gloo":
         device = None   # gloo reduces host tensors
