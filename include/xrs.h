@@ -323,6 +323,8 @@ int xrs_rectify_var(const double* ij, int64_t ij_sn, int64_t dst_h, int64_t dst_
  *                                         pixel floor by the exact division
  *   XRS_TESTING_RECTIFY_MARGIN            k > 1: K5 widens its float32 form margin
  *                                         k-fold (more pixels take the exact test)
+ *   XRS_TESTING_REPROJECT_XCD_GROUP       k > 1: K1b deals k consecutive bands to
+ *                                         an XCD at a time (0 = 1)
  * Returns the previous value (or XRS_ERR_ARG for an unknown knob).
  * ------------------------------------------------------------------------- */
 #define XRS_TESTING_REPROJECT_BAND 1
@@ -330,6 +332,7 @@ int xrs_rectify_var(const double* ij, int64_t ij_sn, int64_t dst_h, int64_t dst_
 #define XRS_TESTING_AFFINE_GENERIC 3
 #define XRS_TESTING_RECTIFY_EXACT 4
 #define XRS_TESTING_RECTIFY_MARGIN 5
+#define XRS_TESTING_REPROJECT_XCD_GROUP 6
 #define XRS_TESTING_NUM_KNOBS 8
 int64_t xrs_testing_set(int knob, int64_t value);
 

@@ -38,12 +38,13 @@ def test_kernel_matches_reference_bitwise(case, interp):
     assert_bitwise_equal(out.cpu().numpy(), g[f"out_{interp}"], f"{case}/{interp}")
 
 
-@pytest.mark.parametrize("band,bpc", [(5, 0), (1, 0), (32, 1), (7, 1)])
-def test_work_shapes_are_bit_identical(band, bpc):
-    """K1's work decomposition (target rows per work item, grid cap) changes
-    only which block computes a pixel: items that split tiles (5 / 1 rows), a
-    single block per CU (grid-stride loop) — all reproduce the reference bit
-    for bit.  The shapes are forced through the test-only knobs
+@pytest.mark.parametrize("band,bpc,group", [(5, 0, 0), (1, 0, 0), (32, 1, 0), (7, 1, 0),
+                                            (8, 0, 4), (3, 1, 2)])
+def test_work_shapes_are_bit_identical(band, bpc, group):
+    """K1's work decomposition (target rows per work item, grid cap, bands an
+    XCD takes in turn) changes only which block computes a pixel: items that
+    split tiles (5 / 1 rows), a single block per CU (grid-stride loop), XCD
+    band groups — all reproduce the reference bit for bit.  The shapes are forced through the test-only knobs
     (xrs_testing_set); the product never reads them from the environment."""
     import torch
 
@@ -59,10 +60,12 @@ def test_work_shapes_are_bit_identical(band, bpc):
                                                                       always_xy=True))
         src = torch.from_numpy(g["data"]).cuda()
         for interp in ("nearest", "bilinear", "triangular"):
-            with testing_knob("reproject_band", band), testing_knob("reproject_blocks_per_cu", bpc):
+            with testing_knob("reproject_band", band), \
+                    testing_knob("reproject_blocks_per_cu", bpc), \
+                    testing_knob("reproject_xcd_group", group):
                 out = kernels.reproject(src, plan, interp, g["fill"].item())
             assert_bitwise_equal(out.cpu().numpy(), g[f"out_{interp}"],
-                                 f"{case}/{interp} band={band} bpc={bpc}")
+                                 f"{case}/{interp} band={band} bpc={bpc} group={group}")
 
 
 @pytest.mark.parametrize("case", NO_DOWNSCALE)

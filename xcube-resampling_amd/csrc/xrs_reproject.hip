@@ -88,6 +88,7 @@ struct Geometry {
   int64_t band;   // target rows per work item of the gathers
   int64_t segw;   // target columns per work item (kThreads x columns per thread)
   int64_t band_first;   // bands of tile row ty0 above row_begin (not in the work list)
+  int64_t xgroup;       // consecutive bands an XCD takes in turn (K1b; 1 in the product)
 };
 
 // numpy fancy index on a window axis of length `win` with an int16 index:
@@ -268,7 +269,7 @@ gather_separable_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t bands_
   const Geometry& g = a.g;
   constexpr int kPx = K1Shape<O>::px, kRows = K1Shape<O>::rows;
   const T fill = Conv<T>::from_f64(a.fill);
-  for (XcdGroups sl = xcd_groups(nwork, nsegs);; sl.i += sl.step) {
+  for (XcdGroups sl = xcd_groups(nwork, nsegs * g.xgroup);; sl.i += sl.step) {
     const int64_t w = sl.item();
     if (w >= nwork) break;
     WorkItem it;
@@ -610,6 +611,8 @@ inline Work work_of(const GatherArgs& a, int64_t band = kBand, int64_t segw = kS
   // them so the tests cover items that split tiles and the grid-stride loop
   const int64_t band_knob = xrs_testing_value(XRS_TESTING_REPROJECT_BAND);
   k.args.g.band = band_knob > 0 ? band_knob : band;
+  const int64_t group_knob = xrs_testing_value(XRS_TESTING_REPROJECT_XCD_GROUP);
+  k.args.g.xgroup = group_knob > 0 ? group_knob : 1;
   k.args.g.segw = segw;
   k.bands_per_tile = (g.tile_h + k.args.g.band - 1) / k.args.g.band;
   k.segs_per_tile = (g.tile_w + k.args.g.segw - 1) / k.args.g.segw;
@@ -766,7 +769,7 @@ extern "C" int xrs_reproject(const void* src, int src_dtype, int64_t n, int64_t 
   g.ntiles_y = (dst_h + tile_h - 1) / tile_h;
   g.src_x = src_x; g.src_y = src_y; g.tile_x0 = tile_x0; g.tile_y0 = tile_y0;
   g.tile_win = tile_win; g.win_h = win_h; g.win_w = win_w;
-  g.x_res = x_res; g.neg_y_res = -y_res; g.err_flags = err_flags; g.band = kBand; g.segw = kSegW; g.band_first = 0;
+  g.x_res = x_res; g.neg_y_res = -y_res; g.err_flags = err_flags; g.band = kBand; g.segw = kSegW; g.band_first = 0; g.xgroup = 1;
   a.src = src; a.n = n; a.src_sn = src_sn; a.src_sy = src_sy;
   a.dst = dst; a.dst_sn = dst_sn; a.dst_sy = dst_sy; a.fill = fill;
   a.xtab = a.ytab = nullptr;
@@ -849,7 +852,7 @@ extern "C" int xrs_reproject_proj(const void* src, int src_dtype, int64_t n, int
   g.ntiles_y = (dst_h + tile_h - 1) / tile_h;
   g.src_x = grid_x; g.src_y = grid_y; g.tile_x0 = tile_x0; g.tile_y0 = tile_y0;
   g.tile_win = tile_win; g.win_h = win_h; g.win_w = win_w;
-  g.x_res = x_res; g.neg_y_res = -y_res; g.err_flags = err_flags; g.band = kBand; g.segw = kSegW; g.band_first = 0;
+  g.x_res = x_res; g.neg_y_res = -y_res; g.err_flags = err_flags; g.band = kBand; g.segw = kSegW; g.band_first = 0; g.xgroup = 1;
   a.src = src; a.n = n; a.src_sn = src_sn; a.src_sy = src_sy;
   a.dst = dst; a.dst_sn = dst_sn; a.dst_sy = dst_sy; a.fill = fill;
   a.xtab = a.ytab = nullptr;
