@@ -925,7 +925,7 @@ rectify_var_kernel(const double* __restrict__ ij, int64_t ij_sn, int64_t dst_h, 
 // column of the item's rows and issues the key loads of all its rows, then the
 // winning quads' corner loads of all its rows, before any arithmetic — three
 // dependent memory round trips per kResolveRows pixels instead of per pixel.
-constexpr int kResolveRows = 4;
+constexpr int kResolveRows = 3;
 
 // A variable sampled by the resolve pass itself (K6 fused into K5b: the
 // first variable of a rectification needs no ij image round trip through HBM).

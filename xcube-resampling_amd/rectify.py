@@ -19,7 +19,7 @@ target offsets).  The pixel work runs on the device:
 
 from __future__ import annotations
 
-from collections.abc import Iterable, Mapping
+from collections.abc import Iterable
 
 import numpy as np
 
@@ -67,14 +67,14 @@ def rectify_dataset(source_ds, target_gm: GridMapping | None = None,
 
     yx_dims = (source_gm.xy_dim_names[1], source_gm.xy_dim_names[0])
     rect_vars = [k for k, v in source_ds.data_vars.items() if v.dims[-2:] == yx_dims]
-    # K6 of the first device-resident nearest-neighbour variable runs inside
-    # K5's resolve pass (xrs_rectify_ij_var); the ij image is kept only for
-    # the others.  Bilinear / triangular sampling is not fused: its taps push
-    # the resolve kernel to 2 waves per SIMD, slower than the two passes
-    # (config 4: 1.50 vs 1.47 ms; nearest 1.36 vs 1.43 ms)
+    # K6 of the first device-resident variable runs inside K5's resolve pass
+    # (xrs_rectify_ij_var); the ij image is kept only for the others.  With
+    # 3 target rows per resolve item the fused pass is quicker for every
+    # interpolation (config 4: nearest 1.30 vs 1.41 ms, bilinear 1.42 vs
+    # 1.45 ms; with 4 rows the bilinear taps cost a wave per SIMD and fusing
+    # it was slower, 1.50 vs 1.47 ms)
     fused = next((k for k in rect_vars if len(source_ds[k].dims) in (2, 3)
-                  and not _streams(source_ds[k].data)
-                  and _is_nearest(interp_methods, k, source_ds[k])), None)
+                  and not _streams(source_ds[k].data)), None)
     if fused is not None:
         da = source_ds[fused]
         src = _var_device(da.data)
@@ -264,18 +264,6 @@ def _device_tiles(source_gm: GridMapping, target_gm: GridMapping, xy):
     return kernels.rectify_tiles_device(
         xy[0], xy[1], target_gm.xy_bboxes, xy_border, 1, grid, (tw, th), (dst_w, dst_h),
         (dst_x_min, dst_y_min, dst_y_max), target_gm.xy_res, target_gm.is_j_axis_up)
-
-
-def _is_nearest(interp_methods, key, var) -> bool:
-    """Whether `var` is sampled nearest-neighbour (utils._get_interp_method's
-    resolution, without its defaults warning: the variable's own pass warns)."""
-    if isinstance(interp_methods, Mapping):
-        m = interp_methods.get(str(key), interp_methods.get(var.dtype))
-    else:
-        m = interp_methods
-    if m is None:
-        m = 0 if np.issubdtype(var.dtype, np.integer) else 1
-    return m in (0, "nearest")
 
 
 def _streams(data) -> bool:
