@@ -148,6 +148,18 @@ TILE_INFO_DTYPE = np.dtype([("r0", np.int32), ("c0", np.int32), ("th", np.int32)
                             ("y_off", np.float64)])
 
 
+def _upload_small(arr: np.ndarray, device, stream):
+    """A small host array on the device.  On the current stream it is staged
+    in page-locked memory and copied asynchronously, so the host does not wait
+    for the work already queued (a pageable copy would drain the queue before
+    every K4); for a side stream the copy stays synchronous, as the kernel on
+    that stream does not wait for the current one."""
+    if stream is None:
+        return torch().from_numpy(np.ascontiguousarray(arr)).pin_memory().to(
+            device, non_blocking=True)
+    return to_device(np.ascontiguousarray(arr), device)
+
+
 def _ij_bboxes_launch(x_image, y_image, xy_bboxes, xy_border, grid, device, stream):
     """Launch K4; returns (device int32 accumulators (n, 4), n, (w, h), grid
     mode used)."""
@@ -166,15 +178,15 @@ def _ij_bboxes_launch(x_image, y_image, xy_bboxes, xy_border, grid, device, stre
         bb = b.reshape(nty, ntx, 4)
         if ntx * nty == n and np.all(bb[:, :, [0, 2]] == bb[:1, :, [0, 2]]) and \
                 np.all(bb[:, :, [1, 3]] == bb[:, :1, [1, 3]]):
-            bx = to_device(np.ascontiguousarray(bb[0, :, [0, 2]].T), device)
-            by = to_device(np.ascontiguousarray(bb[:, 0, [1, 3]]), device)
+            bx = _upload_small(bb[0, :, [0, 2]].T, device, stream)
+            by = _upload_small(bb[:, 0, [1, 3]], device, stream)
         else:
             ntx = nty = 0
     if ntx == 0:
-        bx = to_device(np.ascontiguousarray(b), device)
+        bx = _upload_small(b, device, stream)
         by = bx
-    acc = torch().tensor(np.tile(np.array([[2**31 - 1, 2**31 - 1, -1, -1]], np.int32), (n, 1)),
-                         device=device)
+    acc = _upload_small(np.tile(np.array([[2**31 - 1, 2**31 - 1, -1, -1]], np.int32), (n, 1)),
+                        device, stream)
     rc = _native.lib().xrs_ij_bboxes(ptr(x), ptr(y), h, w, x.stride(0), n, ntx, nty, ptr(bx),
                                      ptr(by), ptr(acc), stream_handle(device, stream))
     _native.check(rc, "xrs_ij_bboxes")
