@@ -4,6 +4,12 @@
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...   (driver, N > 1)
 
+`python bench.py --gpus N` with N > 1 outside torchrun starts the N ranks
+itself: the untouched parent (no GPU call made) runs `python -m
+torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1
+--master-port <free> bench.py <same arguments>` as a child and exits with its
+status (launch_ranks); it refuses N above the visible GPU count.
+
 One "step" = one pass of the hot path (xrs_reproject: K1a axis tables + K1b
 gather) over the rank's share of ONE synthetic 40960^2 raster resident in
 HBM.  Multi-GPU (configs[4]: one raster sharded over the GPUs):
@@ -286,6 +292,38 @@ def shader_clock_ghz(lib, stream, blocks: int = 1024, spin: int = 3000) -> float
     return clock_probe_read(buf)
 
 
+def launch_ranks(n: int, argv: list[str]) -> int:
+    """`--gpus N` (N > 1) from a plain `python bench.py` call: start the N
+    ranks, one process per GPU, under torch.distributed.run as a CHILD of this
+    parent, which has made no GPU call (never an exec after HIP init), and
+    return the child's exit status.  Rank 0 prints the JSON line; stdout and
+    stderr pass through.  With the nccl (RCCL) backend N must not exceed the
+    visible GPUs (torch.cuda.device_count() does not initialise HIP here)."""
+    import socket
+
+    backend = os.environ.get("XRS_BENCH_BACKEND", "nccl")
+    cmd_tail = [os.path.abspath(__file__), *argv]
+    if backend == "nccl" and "--dry-run" not in argv:
+        import torch
+
+        have = torch.cuda.device_count()
+        if have < n:
+            print(f"bench: --gpus {n} needs {n} visible GPUs, found {have}; on an {n}-GPU node "
+                  f"run: python -m torch.distributed.run --nnodes=1 --nproc-per-node {n} "
+                  f"--master-addr 127.0.0.1 --master-port 29500 bench.py {' '.join(argv)}",
+                  file=sys.stderr)
+            return 2
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n}", "--master-addr", "127.0.0.1", f"--master-port={port}",
+           *cmd_tail]
+    env = dict(os.environ, XRS_BENCH_LAUNCHED="1")
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -314,11 +352,21 @@ def main():
                          "fitted in-sample to one-GPU rehearsals: max/mean 1.015 at 8 ranks in "
                          "profiles/r02_band_rehearsal.jsonl; N > 1 lines report every model's "
                          "prediction next to the measured per-rank times)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="host-only rehearsal of the rank logic (launcher, band split, gloo "
+                         "collectives, JSON line with the ranks block): no GPU, no kernel; "
+                         "value and roofline are null")
     args = ap.parse_args()
 
     from xcube_resampling_amd.sharding import band_shard, env_rank, max_over_ranks
 
     rank, world, local_rank = env_rank()
+    if args.gpus > 1 and "RANK" not in os.environ:
+        # a plain `python bench.py --gpus N`: start the N ranks (child processes)
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    dry = args.dry_run
+    if dry:
+        args.no_traffic = args.no_cpu_baseline = args.no_f64 = args.no_graph = True
     # PMC passes first: child processes, before this process initialises HIP
     traffic = None
     if world == 1 and not args.no_traffic:
@@ -336,10 +384,13 @@ def main():
 
     # one GPU per rank; XRS_BENCH_BACKEND=gloo with more ranks than GPUs is only
     # a rehearsal of the multi-rank logic on a smaller box (ranks share GPUs)
-    backend = os.environ.get("XRS_BENCH_BACKEND", "nccl")
-    dev_index = local_rank % torch.cuda.device_count() if backend == "gloo" else local_rank
-    torch.cuda.set_device(dev_index)
-    device = torch.device("cuda", dev_index)
+    backend = "gloo" if dry else os.environ.get("XRS_BENCH_BACKEND", "nccl")
+    if dry:
+        dev_index, device = None, torch.device("cpu")
+    else:
+        dev_index = local_rank % torch.cuda.device_count() if backend == "gloo" else local_rank
+        torch.cuda.set_device(dev_index)
+        device = torch.device("cuda", dev_index)
     # XRS_BENCH_DIST=1: the process group and every collective of the N > 1
     # path also at N = 1 (a one-GPU rehearsal of the RCCL calls the driver's
     # multi-GPU runs make)
@@ -359,14 +410,21 @@ def main():
     else:
         rows, (j0, j1) = (0, plan.dst_height), (0, plan.src_height)
         src = synthetic_rows(0, plan.src_height, args.size, device, seed=20250905 + 1000 * rank)
-    flags = kernels.ErrorFlags(device)
-    benchlib = load_benchlib()
-    stream = torch.cuda.current_stream(device)   # the stream the kernels run on
+    flags = None if dry else kernels.ErrorFlags(device)
+    benchlib = None if dry else load_benchlib()
+    # the stream the kernels run on
+    stream = None if dry else torch.cuda.current_stream(device)
     copy_rates = []
+
+    def sync():
+        if not dry:
+            torch.cuda.synchronize()
 
     def make_step(out, dtype):
         def step():
-            if rows[1] > rows[0]:
+            if dry:
+                out.zero_()          # host stand-in: the rehearsal times no kernel
+            elif rows[1] > rows[0]:
                 kernels.reproject(src, plan, "bilinear", float("nan"), out_dtype=dtype, out=out,
                                   rows=rows, src_row0=j0, flags=flags, check=False)
         return step
@@ -389,38 +447,48 @@ def main():
                 step()
             run = g.replay
         barrier()   # the first collective sets the communicator up: not between warm-up and timing
-        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        # the same-run device-copy rate, measured back to back with the warm-up
-        # steps: its ~0.1 s of streaming also takes the shader clock to its
-        # loaded level (DVFS: ~30 ms of load from idle), as W steps alone may not
-        copy_rates.append(device_copy_rate(benchlib, src, stream))
+        if not dry:
+            ev0 = torch.cuda.Event(enable_timing=True)
+            ev1 = torch.cuda.Event(enable_timing=True)
+            # the same-run device-copy rate, measured back to back with the warm-up
+            # steps: its ~0.1 s of streaming also takes the shader clock to its
+            # loaded level (DVFS: ~30 ms of load from idle), as W steps alone may not
+            copy_rates.append(device_copy_rate(benchlib, src, stream))
+        else:
+            copy_rates.append(0.0)
         for _ in range(warmup):
             run()
         # nothing on the host between the warm-up and the timed steps but the
         # barrier and the synchronize: an idle gap of a few ms lets the clock
         # drop, and the first timed launches ramp up again (kernel trace of
         # r03's first version: 17.6 ms of host work here, then 3.0 -> 2.5 ms)
-        probe0 = clock_probe_launch(benchlib, stream)   # read after the timed steps
-        torch.cuda.synchronize()   # every rank's own queue drained ...
-        barrier()                  # ... before the ranks start together
-        torch.cuda.synchronize()
+        probe0 = None if dry else clock_probe_launch(benchlib, stream)   # read after timing
+        sync()      # every rank's own queue drained ...
+        barrier()   # ... before the ranks start together
+        sync()
         t0 = time.perf_counter()
-        ev0.record(stream)
+        if not dry:
+            ev0.record(stream)
         for _ in range(steps):
             run()
-        ev1.record(stream)
-        torch.cuda.synchronize()
+        if not dry:
+            ev1.record(stream)
+        sync()
+        t_own = time.perf_counter() - t0
         barrier()
         t1 = time.perf_counter()
+        wall = max_over_ranks(t1 - t0, device) / steps * 1e3
+        if dry:
+            return wall, t_own / steps * 1e3, (None, None)
         clk0 = clock_probe_read(probe0)
         clk1 = shader_clock_ghz(benchlib, stream)
-        wall = max_over_ranks(t1 - t0, device) / steps * 1e3
         return wall, ev0.elapsed_time(ev1) / steps, (clk0, clk1)
 
     out = torch.empty((1, rows[1] - rows[0], args.size), device=device,
                       dtype=torch.float32 if out_np == np.float32 else torch.float64)
     ms_per_step, kernel_ms, clocks = timed(make_step(out, out_np), args.steps, args.warmup)
-    flags.raise_if_set("bench reproject")
+    if flags is not None:
+        flags.raise_if_set("bench reproject")
 
     copy_gbs = copy_rates[0]
     s_read = source_pixels_read(plan, rows) if rows[1] > rows[0] else 0
@@ -505,13 +573,18 @@ def main():
                 "kernel_ms": round(max_kernel_ms, 4),
                 "algorithmic_bytes": int(alg_bytes),
                 "copy_GBs": round(copy_all, 1),
-                "frac_of_copy": round(achieved / copy_all, 4),
+                "frac_of_copy": round(achieved / copy_all, 4) if copy_all > 0 else None,
                 "copy": "same-run streaming float4 copy of each rank's source band (read + "
                         "write bytes / time; benchlib xrs_bench_copy), summed over ranks",
                 "scope": "whole job: bytes of all ranks / slowest rank's kernel time; "
                          "peak = n_gpus x 8 TB/s",
             },
         }
+        if dry:   # nothing above was measured on a GPU
+            res["value"] = None
+            res["roofline"] = None
+            res["dry_run"] = ("host-only rehearsal (--dry-run): launcher, band split, gloo "
+                              "collectives and the ranks block; no GPU, no kernel")
         res["clock_GHz"] = {"before_timed": clocks[0], "after_timed": clocks[1],
                             "note": "rank 0 shader clock (s_memtime / s_memrealtime probe) "
                                     "right outside the timed region"}

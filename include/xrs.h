@@ -72,8 +72,14 @@ const char* xrs_last_error(void);
  * reproject.py:254-255, affine.py:227-228): page-lock a caller-owned host
  * buffer in place so band-wise H2D / D2H copies run as DMA on their own
  * streams, overlapped with the kernels (xcube_resampling_amd/streaming.py).
- * xrs_host_register returns XRS_OK, or 1 when the range was already
- * registered (the caller must then NOT unregister it), or XRS_ERR_HIP.
+ * The engine itself stages through its own page-locked buffers; these two
+ * are for bindings that own long-lived, page-aligned buffers (mmap /
+ * posix_memalign).  xrs_host_register accepts only whole pages: `ptr` on a
+ * page boundary and `bytes` a multiple of the page size (else XRS_ERR_ARG —
+ * a malloc'd numpy array shares its edge pages with its neighbours); returns
+ * XRS_OK, 1 when the range was already registered (the caller must then NOT
+ * unregister it), or XRS_ERR_HIP.  xrs_host_unregister drains the device
+ * (every stream) before unpinning, so no queued copy outlives the pinning.
  * ------------------------------------------------------------------------- */
 int xrs_host_register(void* ptr, int64_t bytes);
 int xrs_host_unregister(void* ptr);

@@ -80,3 +80,46 @@ def test_pmc_traffic_reduce(tmp_path):
     assert np.isclose(r["calibration"]["fetch_factor"], 2.0)
     assert r["read_bytes"] == int(3000.0 * 1024 * 2.0)
     assert r["write_bytes"] == int(3906.25 * 1024)
+
+
+def _run_bench(args, env_extra=None, timeout=240):
+    import json
+    import subprocess
+    import sys
+
+    from conftest import ROOT
+
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", **(env_extra or {}))
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], env=env,
+                       cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                       timeout=timeout)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    return r, (json.loads(lines[-1]) if lines else None)
+
+
+def test_gpus_flag_launches_the_ranks_itself():
+    """`python bench.py --gpus 2` outside torchrun starts 2 ranks itself
+    (torch.distributed.run child of the untouched parent); host-only
+    rehearsal (--dry-run, gloo): ONE JSON line from rank 0 with n_gpus 2, the
+    ranks block (both ranks' times, the cuts, every balance model's
+    prediction) and no measured value."""
+    r, line = _run_bench(["--gpus", "2", "--dry-run", "--size", "2048", "--tile", "512",
+                          "--steps", "2", "--warmup", "1"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert sum(ln.startswith("{") for ln in r.stdout.splitlines()) == 1
+    assert line["n_gpus"] == 2 and line["config"]["parallelism"] == "bands2"
+    assert len(line["ranks"]["kernel_ms"]) == 2
+    cuts = line["ranks"]["cuts"]
+    assert cuts[0] == 0 and cuts[-1] == 2048 and len(cuts) == 3
+    assert set(line["ranks"]["predicted"]) == {"rows", "bytes", "cost"}
+    assert line["value"] is None and line["roofline"] is None and "dry_run" in line
+
+
+def test_gpus_flag_refuses_more_ranks_than_gpus():
+    """Without enough visible GPUs (none here) `--gpus 4` exits non-zero with
+    the exact torchrun command instead of measuring one GPU."""
+    r, line = _run_bench(["--gpus", "4", "--steps", "1", "--warmup", "0"], timeout=120)
+    assert r.returncode == 2 and line is None
+    assert "--nproc-per-node 4" in r.stderr and "--master-addr 127.0.0.1" in r.stderr

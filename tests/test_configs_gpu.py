@@ -72,7 +72,9 @@ def test_config2_reproject_bilinear_8192_f64():
 
 
 @pytest.mark.parametrize("interp", ["nearest", "triangular"])
-def test_config2_other_methods_sampled(interp):
+def test_config2_other_methods_all_tiles(interp):
+    """Config 2 nearest / triangular through the K1 launch: ALL 16 tiles
+    against the oracle's block on the oracle's window."""
     import torch
 
     from xcube_resampling_amd import kernels
@@ -86,7 +88,9 @@ def test_config2_other_methods_sampled(interp):
     src = torch.rand((1, size, size), generator=gen, device="cuda", dtype=torch.float32)
     out = kernels.reproject(src, plan, interp, float("nan"))
     host = lambda j0, j1, i0, i1: src[:, j0:j1, i0:i1].cpu().numpy()  # noqa: E731
-    for j, i in [(0, 0), (1, 2), (3, 3)]:
+    tiles = [(j, i) for j in range(o["nty"]) for i in range(o["ntx"])]
+    assert len(tiles) == 16
+    for j, i in tiles:
         ref, (r0, r1, c0, c1) = configs.oracle_tile(o, host, j, i, interp)
         assert_bitwise_equal(out[:, r0:r1, c0:c1].cpu().numpy(), ref, f"{interp} ({j}, {i})")
 

@@ -115,3 +115,28 @@ def test_library_override_limited_to_probe_arms(tmp_path):
         out = subprocess.run([sys.executable, "-c", code], env=env, cwd=root,
                              capture_output=True, text=True, timeout=120).stdout
         assert out.startswith(expect), out
+
+
+def test_host_register_refuses_partial_pages():
+    """xrs_host_register accepts whole pages only: an array
+    that starts inside a page (numpy's malloc'd buffers do) or a size that is
+    not a page multiple is refused with XRS_ERR_ARG before any HIP call."""
+    import ctypes
+    import mmap
+
+    from xcube_resampling_amd import _native
+
+    lib = _native.load_library()
+    page = mmap.PAGESIZE
+    buf = mmap.mmap(-1, 4 * page)
+    base = ctypes.addressof(ctypes.c_char.from_buffer(buf))
+    try:
+        assert base % page == 0
+        for ptr, size in [(base + 16, page), (base, page + 8), (base, 100)]:
+            assert lib.xrs_host_register(ctypes.c_void_p(ptr), size) == _native.XRS_ERR_ARG
+            assert "page" in _native.last_error()
+        assert lib.xrs_host_register(None, page) == _native.XRS_ERR_ARG
+        assert lib.xrs_host_unregister(None) == _native.XRS_ERR_ARG
+    finally:
+        del base
+        buf.close()

@@ -338,9 +338,10 @@ def test_fused_resolve_sampling_equals_k5_then_k6(dtype, interp, n, keep_ij):
 
 
 def test_rectify_dataset_fused_first_variable():
-    """rectify_dataset samples its first nearest-neighbour device variable
-    inside K5: one and two variables, nearest, bilinear and mixed, give the
-    same values as each variable rectified alone."""
+    """rectify_dataset samples its first device variable inside K5's resolve
+    pass whatever its interpolation (rectify.py fuses nearest, bilinear and
+    triangular alike): one and two variables, nearest, bilinear and mixed,
+    give the same values as each variable rectified alone."""
     import xcube_resampling_amd as xrs
 
     rng = np.random.default_rng(3)
@@ -435,10 +436,29 @@ def test_config4_full_size_matches_oracle():
     assert_bitwise_equal(ij.cpu().numpy(), exp_ij, "ij")
     assert np.sum(~np.isnan(exp_ij[0])) > 30_000_000
     src = torch.from_numpy(var).cuda()
+    # the fused pass (K6 inside K5's resolve) is what rectify_dataset runs for
+    # its first variable and what the config-4 line times: oracle-pinned here
+    # on the whole swath too, keeping the ij image and not
+    import xcube_resampling_amd as xrs
+    from xcube_resampling_amd import rectify as R
+
+    tgm = xrs.GridMapping.regular(size, (x0, y0), res, "EPSG:4326", tile_size=tile)
+    sgm = xrs.GridMapping.from_coords(xrs.DataArray(lon, ("y", "x"), name="lon"),
+                                      xrs.DataArray(lat, ("y", "x"), name="lat"), "EPSG:4326")
+    xy = (torch.from_numpy(lon).cuda(), torch.from_numpy(lat).cuda())
+    dev_tiles = R._device_tiles(sgm, tgm, xy)
     for interp in ("nearest", "bilinear"):
         exp = rectify_ref.compute_var_image(exp_ij, var, np.nan, interp, tile, threads=16)
         assert_bitwise_equal(kernels.rectify_var(ij, src, interp, np.nan).cpu().numpy(), exp,
                              interp)
+        for keep_ij in (False, True):
+            ij2, got = kernels.rectify_ij_var(xy[0], xy[1], dev_tiles, tgm.height, tgm.width,
+                                              tgm.x_res, -tgm.y_res, 1e-3, src, interp, np.nan,
+                                              keep_ij=keep_ij)
+            assert_bitwise_equal(got.cpu().numpy(), exp, f"fused {interp} keep_ij={keep_ij}")
+            if keep_ij:
+                assert_bitwise_equal(ij2.cpu().numpy(), exp_ij, "fused ij")
+            del ij2, got
 
 
 def test_nan_cornered_quads_on_untiled_large_target():

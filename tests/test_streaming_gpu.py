@@ -237,4 +237,86 @@ def test_staging_round_trip_multi_chunk():
             back = streaming.device_to_host(d)
             assert back.dtype == a.dtype
             assert np.array_equal(back.view(np.uint8), np.ascontiguousarray(a).view(np.uint8))
-    assert streaming._STAGING is not None and len(streaming._STAGING.bufs) == 2
+    assert streaming._staging() is streaming._staging()
+    assert len(streaming._staging().bufs) == 2
+
+
+def test_staging_concurrent_threads():
+    """Streamed copies from several host threads at once (a threaded chunk
+    scheduler calling the dataset APIs): each thread stages through its own
+    page-locked pair, so no thread's bytes land in another's array."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    import torch
+
+    from xcube_resampling_amd import streaming
+    from xcube_resampling_amd.options import set_options
+
+    import threading
+
+    n = 2 * (streaming._STAGE_BYTES // 4) + 999
+    start = threading.Barrier(4, timeout=60)   # four distinct threads, copying together
+
+    def work(k):
+        torch.cuda.set_device(0)
+        start.wait()
+        a = np.random.default_rng(100 + k).random(n, dtype=np.float32)
+        ok = True
+        for _ in range(3):
+            d = streaming.host_to_device(a, "cuda:0")
+            ok &= np.array_equal(streaming.device_to_host(d), a)
+        return ok, id(streaming._staging())
+
+    with set_options(host_streaming_min_bytes=0), ThreadPoolExecutor(4) as ex:
+        res = list(ex.map(work, range(4)))
+    assert all(ok for ok, _ in res)
+    assert len({i for _, i in res}) == 4
+
+
+def test_host_register_copy_unregister_then_fresh_pageable_copy():
+    """The sequence behind round 3's illegal-address faults:
+    register a page-aligned host buffer -> async copy to the device ->
+    unregister -> free the pages -> a fresh allocation of the same size (the
+    kernel usually hands back the same addresses) -> a pageable copy from it.
+    Every copy lands the bytes it was given; a malloc'd numpy array is
+    refused."""
+    import ctypes
+    import mmap
+
+    import torch
+
+    from xcube_resampling_amd import _native
+
+    lib = _native.lib()
+    page = mmap.PAGESIZE
+    nbytes = 64 * (1 << 20)
+    assert nbytes % page == 0
+    dev = torch.empty(nbytes // 4, dtype=torch.float32, device="cuda")
+    stream = torch.cuda.current_stream()
+    rng = np.random.default_rng(4)
+    addrs = []
+    for k in range(3):
+        buf = mmap.mmap(-1, nbytes)
+        host = np.frombuffer(buf, dtype=np.float32)
+        host[:] = rng.random(host.size, dtype=np.float32)
+        ptr = host.ctypes.data
+        addrs.append(ptr)
+        assert ptr % page == 0
+        assert lib.xrs_host_register(ctypes.c_void_p(ptr), nbytes) == _native.XRS_OK
+        _native.check(lib.xrs_copy_async(ctypes.c_void_p(dev.data_ptr()), ctypes.c_void_p(ptr),
+                                         nbytes, ctypes.c_void_p(stream.cuda_stream)),
+                      "xrs_copy_async")
+        _native.check(lib.xrs_host_unregister(ctypes.c_void_p(ptr)), "xrs_host_unregister")
+        expect = host.copy()
+        assert_bitwise_equal(dev.cpu().numpy(), expect, f"registered copy {k}")
+        del host
+        buf.close()                                  # the pages go back to the kernel
+        fresh = np.frombuffer(mmap.mmap(-1, nbytes), dtype=np.float32)
+        fresh[:] = rng.random(fresh.size, dtype=np.float32)
+        got = torch.from_numpy(fresh).cuda()         # pageable copy from the fresh range
+        assert_bitwise_equal(got.cpu().numpy(), fresh, f"pageable copy after unregister {k}")
+        del got, fresh
+    heap = np.empty(nbytes // 4 + 3, np.float32)     # malloc'd: starts inside a page
+    if heap.ctypes.data % page:
+        assert lib.xrs_host_register(ctypes.c_void_p(heap.ctypes.data),
+                                     heap.nbytes) == _native.XRS_ERR_ARG

@@ -2,7 +2,10 @@
 // behind xrs_last_error() (include/xrs.h).
 #include <atomic>
 #include <cstdarg>
+#include <cstdint>
 #include <cstdio>
+
+#include <unistd.h>
 
 #include <hip/hip_runtime.h>
 
@@ -36,9 +39,26 @@ extern "C" const char* xrs_version(void) { return "xrs 0.1.0 (gfx950)"; }
 
 extern "C" const char* xrs_last_error(void) { return g_last_error; }
 
+// Page-locking is page-granular: the runtime pins (and later unpins) every
+// page the range touches.  A range that does not start and end on page
+// boundaries shares its first / last page with whatever the allocator put
+// beside it (a numpy array from malloc starts 16 bytes into an mmap page, or
+// inside the brk heap below glibc's dynamic mmap threshold of up to 32 MiB),
+// so two registrations can cover one page and unregistering one changes the
+// pinning of memory the other — or a later allocation reusing the freed
+// range — still relies on.  Only whole pages the caller owns are accepted
+// (DESIGN.md §2).
 extern "C" int xrs_host_register(void* ptr, int64_t bytes) {
+  const int64_t page = (int64_t)sysconf(_SC_PAGESIZE);
   if (!ptr || bytes <= 0) {
     xrs_set_error("xrs_host_register: invalid argument");
+    return XRS_ERR_ARG;
+  }
+  if (reinterpret_cast<uintptr_t>(ptr) % (uintptr_t)page != 0 || bytes % page != 0) {
+    xrs_set_error("xrs_host_register: the range must start on a page boundary and span whole "
+                  "pages (%lld-byte pages; got offset %lld, %lld bytes)", (long long)page,
+                  (long long)(reinterpret_cast<uintptr_t>(ptr) % (uintptr_t)page),
+                  (long long)bytes);
     return XRS_ERR_ARG;
   }
   const hipError_t e = hipHostRegister(ptr, (size_t)bytes, hipHostRegisterDefault);
@@ -59,7 +79,16 @@ extern "C" int xrs_host_unregister(void* ptr) {
     xrs_set_error("xrs_host_unregister: invalid argument");
     return XRS_ERR_ARG;
   }
-  const hipError_t e = hipHostUnregister(ptr);
+  // A copy queued on any stream (the band pipelines use three) may still
+  // read or write the range: drain the device before the pages are unpinned,
+  // so no DMA outlives the registration it was issued under.
+  hipError_t e = hipDeviceSynchronize();
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    xrs_set_error("xrs_host_unregister: hipDeviceSynchronize: %s", hipGetErrorString(e));
+    return XRS_ERR_HIP;
+  }
+  e = hipHostUnregister(ptr);
   if (e != hipSuccess) {
     (void)hipGetLastError();
     xrs_set_error("hipHostUnregister: %s", hipGetErrorString(e));

@@ -190,6 +190,12 @@ def _ij_bboxes_launch(x_image, y_image, xy_bboxes, xy_border, grid, device, stre
     rc = _native.lib().xrs_ij_bboxes(ptr(x), ptr(y), h, w, x.stride(0), n, ntx, nty, ptr(bx),
                                      ptr(by), ptr(acc), stream_handle(device, stream))
     _native.check(rc, "xrs_ij_bboxes")
+    if stream is not None:
+        # made on the current stream, read (acc: written) by K4 on `stream`:
+        # bx / by (and uploaded coordinates) are freed when this returns, so
+        # keep their memory from the allocator until `stream` is past K4
+        for t in (x, y, bx, by, acc):
+            t.record_stream(stream)
     return acc, n, (w, h), ntx > 0
 
 

@@ -21,6 +21,7 @@ to the resident path: the same K1 launch, restricted to the band's rows.
 from __future__ import annotations
 
 import ctypes
+import threading
 
 import numpy as np
 
@@ -131,14 +132,20 @@ class _Staging:
                 self.events[i] = None
 
 
-_STAGING = None
+_STAGING = threading.local()
 
 
 def _staging() -> _Staging:
-    global _STAGING
-    if _STAGING is None:
-        _STAGING = _Staging()
-    return _STAGING
+    """This thread's staging buffers.  A _Staging holds shared state (the
+    buffer index, the events of the DMAs still using each buffer) that two
+    threads must not interleave — a threaded chunk scheduler calling the
+    dataset APIs from several threads would overwrite each other's staged
+    bytes — so every thread that streams gets its own pair (allocated on its
+    first streamed copy, 2 x 16 MiB page-locked)."""
+    st = getattr(_STAGING, "st", None)
+    if st is None:
+        st = _STAGING.st = _Staging()
+    return st
 
 
 def host_to_device(arr, device, dtype=None):
