@@ -30,8 +30,9 @@ the clock measured just before and just after the timed steps.
 `roofline.achieved` = algorithmic bytes of all ranks (output + distinct
 source pixels read, x4 B) / max-over-ranks kernel time (HIP events on the
 launch stream); `peak` = N x 8 TB/s.  `traffic` = FETCH_SIZE + WRITE_SIZE per
-launch measured by two rocprofv3 --pmc child passes of this workload before
-the bench touches the GPU (N = 1; calibrated, scripts/pmc_traffic.py).
+launch from two rocprofv3 --pmc child passes of this workload before the
+bench touches the GPU (N = 1): the L2's memory-side requests counted by size,
+with three launches of known bytes beside it (scripts/pmc_traffic.py).
 Rank 0 prints ONE JSON line.
 """
 
@@ -192,12 +193,16 @@ def cpu_baseline(plan, tgm, seconds: float = 12.0, sweep=(1, 32, 128), sweep_sec
 
 
 def measure_traffic(size: int, tile: int, out_dtype: str, timeout: int = 170):
-    """HBM bytes per launch from two rocprofv3 --pmc child passes (FETCH_SIZE,
-    WRITE_SIZE: separate passes, MI355X_MICROARCH.md §rocprofv3 PMC slots) of
-    scripts/pmc_traffic.py on this workload, FETCH_SIZE calibrated on an
-    identity launch of the same access pattern.  Must run before this
-    process touches the GPU (the children are separate processes).  Returns
-    the reduced dict or None (no rocprofv3, or a pass failed)."""
+    """HBM bytes per launch from two rocprofv3 --pmc child passes of
+    scripts/pmc_traffic.py on this workload (separate passes within the TCC
+    block's 4 counter slots, MI355X_MICROARCH.md §rocprofv3 PMC): read bytes
+    from the size-resolved L2 -> memory requests (32 / 64 / 128 B), write
+    bytes from the 32 / 64 B write requests — no correction factor; a float4
+    copy, a 4-byte-lane copy and an identity K1 launch of known bytes run in
+    the same process and are reported beside it (measured / known).  Must run
+    before this process touches the GPU (the children are separate
+    processes).  Returns the reduced dict or None (no rocprofv3, or a pass
+    failed)."""
     prof = shutil.which("rocprofv3")
     if prof is None:
         return None
@@ -206,19 +211,19 @@ def measure_traffic(size: int, tile: int, out_dtype: str, timeout: int = 170):
 
     d = tempfile.mkdtemp(prefix="xrs_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
     env = dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp"))
-    for counter, name in (("FETCH_SIZE", "fetch"), ("WRITE_SIZE", "write")):
-        cmd = ["timeout", "-s", "KILL", str(timeout), prof, "--pmc", counter, "--kernel-trace",
+    for name, counters in pmc_traffic.PASSES.items():
+        cmd = ["timeout", "-s", "KILL", str(timeout), prof, "--pmc", *counters, "--kernel-trace",
                "--output-format", "csv", "-d", os.path.join(d, name), "-o", name, "--",
                sys.executable, os.path.join(ROOT, "scripts", "pmc_traffic.py"), "--size",
                str(size), "--tile", str(tile), "--out-dtype", out_dtype]
         r = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
                            text=True)
         if r.returncode != 0:
-            print(f"bench: rocprofv3 {counter} pass failed (rc {r.returncode}):\n"
+            print(f"bench: rocprofv3 pass {name} failed (rc {r.returncode}):\n"
                   f"{r.stdout[-2000:]}", file=sys.stderr)
             return None
     try:
-        return pmc_traffic.reduce(d, size, out_dtype, write=False)
+        return pmc_traffic.reduce(d, size, out_dtype)
     except Exception as e:   # a missing / malformed counter file: report null traffic
         print(f"bench: PMC reduce failed: {e}", file=sys.stderr)
         return None
@@ -600,6 +605,11 @@ def main():
         if traffic:
             res["roofline"]["traffic_detail"] = {
                 k: traffic[k] for k in ("read_bytes", "write_bytes", "calibration")}
+            res["roofline"]["traffic_detail"]["read_over_algorithmic"] = round(
+                traffic["read_bytes"] / (4 * s_read), 4) if s_read else None
+            res["roofline"]["traffic_detail"]["requests"] = {
+                k: traffic["launches"]["bench"][k] for k in ("rdreq", "rdreq_dram", "wrreq",
+                                                             "wrreq_64B")}
         if secondary:
             res["f64_out"] = secondary
         if cpu is not None:

@@ -60,6 +60,61 @@ __global__ void __launch_bounds__(256) copy_unrolled_kernel(const f32x4* __restr
   }
 }
 
+// 4-byte lanes (traffic calibration): one block per 256 x U floats, lane l of
+// each of the U rounds moves float (round * 256 + l) — every wave instruction
+// reads / writes 256 contiguous bytes, the width of K1's dword taps.
+template <int U>
+__global__ void __launch_bounds__(256) copy_b32_kernel(const float* __restrict__ src,
+                                                       float* __restrict__ dst, int64_t n) {
+  const int64_t base = (int64_t)blockIdx.x * 256 * U + threadIdx.x;
+  float v[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t i = base + u * 256;
+    if (i < n) v[u] = src[i];
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t i = base + u * 256;
+    if (i < n) dst[i] = v[u];
+  }
+}
+
+// XCD-placement probe (diagnostic): block b copies chunk (b / 8) * 8 +
+// (b % 8 + shift) % 8 of `chunk` bytes, i.e. rotates which of the 8 XCDs
+// (blocks are dealt to them round-robin) moves which chunk of every group of
+// 8: a time that depends on `shift` means the memory behind an address is
+// nearer to some XCDs than to others at that granularity.
+__global__ void __launch_bounds__(256) xcd_copy_kernel(const f32x4* __restrict__ src,
+                                                       f32x4* __restrict__ dst, int64_t n4,
+                                                       int64_t q, int shift) {
+  const int64_t b = blockIdx.x;
+  const int64_t c = (b >> 3) * 8 + (((b & 7) + shift) & 7);
+  const int64_t base = c * q * 256 + threadIdx.x;
+  for (int64_t u = 0; u < q; u += 4) {
+    f32x4 v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int64_t i = base + (u + k) * 256;
+      if (u + k < q && i < n4) v[k] = src[i];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int64_t i = base + (u + k) * 256;
+      if (u + k < q && i < n4) dst[i] = v[k];
+    }
+  }
+}
+
+extern "C" int xrs_bench_xcd_copy(const void* src, void* dst, int64_t bytes, int64_t chunk,
+                                  int shift, void* stream) {
+  if (bytes % chunk || chunk % 4096 || (bytes / chunk) % 8) return -1;
+  const int64_t q = chunk / 4096;   // float4s per thread
+  hipLaunchKernelGGL(xcd_copy_kernel, dim3((unsigned)(bytes / chunk)), dim3(256), 0,
+                     (hipStream_t)stream, (const f32x4*)src, (f32x4*)dst, bytes / 16, q, shift);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 // Region copy in K1's work shape (diagnostic): a (rows x cols) f32 image cut
 // into items of `band` rows x `segw` columns; one item per block, its float4s
 // walked row-major by the 256 threads, RIF loads in flight before their stores.
@@ -197,7 +252,8 @@ extern "C" int xrs_bench_clock_probe(void* out, int blocks, int spin, void* stre
 }
 
 // variant: 0 grid-stride nt (4096 blocks), 1 grid-stride plain, 2 unroll-1 plain,
-// 3 unroll-4 plain, 4 unroll-4 nt, 5 unroll-8 plain, 6 unroll-8 nt
+// 3 unroll-4 plain, 4 unroll-4 nt, 5 unroll-8 plain, 6 unroll-8 nt,
+// 7 4-byte lanes (8 floats per thread in flight)
 extern "C" int xrs_bench_copy(const void* src, void* dst, int64_t bytes, int variant,
                               void* stream) {
   if (bytes % 16 != 0 || ((uintptr_t)src | (uintptr_t)dst) % 16 != 0) return -1;
@@ -214,6 +270,10 @@ extern "C" int xrs_bench_copy(const void* src, void* dst, int64_t bytes, int var
     case 4: hipLaunchKernelGGL((copy_unrolled_kernel<4, true>), blocks(4), dim3(256), 0, st, s, d, n4); break;
     case 5: hipLaunchKernelGGL((copy_unrolled_kernel<8, false>), blocks(8), dim3(256), 0, st, s, d, n4); break;
     case 6: hipLaunchKernelGGL((copy_unrolled_kernel<8, true>), blocks(8), dim3(256), 0, st, s, d, n4); break;
+    case 7:
+      hipLaunchKernelGGL((copy_b32_kernel<8>), dim3((unsigned)((bytes / 4 + 2047) / 2048)), dim3(256),
+                         0, st, (const float*)src, (float*)dst, bytes / 4);
+      break;
     default: return -1;
   }
   return hipGetLastError() == hipSuccess ? 0 : -1;

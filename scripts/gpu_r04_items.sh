@@ -14,5 +14,15 @@ tail -3 $OUT/pytest_items.log
 rc=0
 timeout -k 10 120 python -u bench.py --gpus 2 --steps 2 --warmup 1 > $OUT/bench_g2.json 2> $OUT/bench_g2.err || rc=$?
 echo "bench --gpus 2 on one GPU: rc=$rc"; tail -2 $OUT/bench_g2.err
-timeout -k 10 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline > $OUT/bench_g1.json 2> $OUT/bench_g1.err || exit $?
+timeout -k 10 500 python -u bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline > $OUT/bench_g1.json 2> $OUT/bench_g1.err || exit $?
 cut -c1-300 $OUT/bench_g1.json
+python -c "import json,sys; d=json.load(open(sys.argv[1])); print(json.dumps(d['roofline']))" $OUT/bench_g1.json
+timeout -k 10 200 python -u scripts/xcd_probe.py > $OUT/xcd_probe.jsonl 2> $OUT/xcd_probe.err || exit $?
+python - $OUT/xcd_probe.jsonl <<'PY'
+import json, sys, collections
+d = collections.defaultdict(list)
+for l in open(sys.argv[1]):
+    r = json.loads(l); d[r["chunk"]].append(r["GBs"])
+for k, v in d.items():
+    print(k, min(v), max(v))
+PY

@@ -55,31 +55,49 @@ def test_split_predictions_report_every_model():
 
 
 def test_pmc_traffic_reduce(tmp_path):
-    """Two gather dispatches per pass (calibration, bench); FETCH_SIZE is
-    scaled by the identity launch's known 4*S bytes."""
+    """Read / write bytes from the size-resolved request counters, per launch
+    (two copies, then two gather dispatches: identity calibration, bench),
+    instances summed; the calibration launches are reported as measured /
+    known bytes, without any correction of the bench numbers."""
     import sys
 
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(__file__)), "scripts"))
     import pmc_traffic
 
     size = 1000
-    for name, counter, vals in (("fetch", "FETCH_SIZE", (4 * size * size / 2 / 1024, 3000.0)),
-                                ("write", "WRITE_SIZE", (4 * size * size / 1024, 3906.25))):
-        d = tmp_path / name
+    nb = 4 * size * size
+    # per launch (copy16, copy4, ident, bench): (n32, n64, n128), (wr, wr64), dram
+    rd = {"copy16": (0, 0, nb // 128), "copy4": (0, 10, nb // 128 - 5),
+          "ident": (0, 2, nb // 128 - 1), "bench": (4, 100, 40000)}
+    wr = {"copy16": (nb // 64, nb // 64), "copy4": (nb // 64, nb // 64),
+          "ident": (nb // 64, nb // 64), "bench": (nb // 64 + 8, nb // 64)}
+    kname = {"copy16": "copy_unrolled_kernel<1, false>", "copy4": "copy_b32_kernel<8>",
+             "ident": "gather_separable_kernel<...>", "bench": "gather_separable_kernel<...>"}
+    for p, counters in pmc_traffic.PASSES.items():
+        d = tmp_path / p
         d.mkdir()
-        with open(d / f"{name}_counter_collection.csv", "w", newline="") as f:
+        with open(d / f"{p}_counter_collection.csv", "w", newline="") as f:
             w = csv.DictWriter(f, ["Dispatch_Id", "Kernel_Name", "Counter_Name", "Counter_Value"])
             w.writeheader()
-            for did, v in enumerate(vals, start=1):
-                for half in (0.5, 0.5):   # two instances per dispatch are summed
-                    w.writerow(dict(Dispatch_Id=did, Kernel_Name="gather_separable_kernel<...>",
-                                    Counter_Name=counter, Counter_Value=v * half))
+            for did, launch in enumerate(pmc_traffic.LAUNCHES, start=1):
+                n32, n64, n128 = rd[launch]
+                vals = {"TCC_EA0_RDREQ_sum": n32 + n64 + n128, "TCC_EA0_RDREQ_32B_sum": n32,
+                        "TCC_EA0_RDREQ_64B_sum": n64, "TCC_EA0_RDREQ_128B_sum": n128,
+                        "TCC_EA0_WRREQ_sum": wr[launch][0], "TCC_EA0_WRREQ_64B_sum": wr[launch][1],
+                        "TCC_EA0_RDREQ_DRAM_sum": 7}
+                for c in counters:
+                    for half in (0.5, 0.5):   # two instances per dispatch are summed
+                        w.writerow(dict(Dispatch_Id=did, Kernel_Name=kname[launch],
+                                        Counter_Name=c, Counter_Value=vals[c] * half))
                 w.writerow(dict(Dispatch_Id=did + 10, Kernel_Name="axis_tables_kernel<1>",
-                                Counter_Name=counter, Counter_Value=1e9))
+                                Counter_Name=counters[0], Counter_Value=1e9))
     r = pmc_traffic.reduce(str(tmp_path), size, "f32", write=False)
-    assert np.isclose(r["calibration"]["fetch_factor"], 2.0)
-    assert r["read_bytes"] == int(3000.0 * 1024 * 2.0)
-    assert r["write_bytes"] == int(3906.25 * 1024)
+    assert r["read_bytes"] == 4 * 32 + 100 * 64 + 40000 * 128
+    assert r["write_bytes"] == (nb // 64) * 64 + 8 * 32
+    assert r["launches"]["copy16"]["read_over_known"] == 1.0
+    assert r["launches"]["copy4"]["read_over_known"] == round((640 + nb - 640) / nb, 4)
+    assert r["launches"]["bench"]["rdreq_dram"] == 7
+    assert r["hbm_bytes_per_launch"] == r["read_bytes"] + r["write_bytes"]
 
 
 def _run_bench(args, env_extra=None, timeout=240):

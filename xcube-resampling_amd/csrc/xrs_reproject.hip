@@ -65,6 +65,7 @@ struct K1Shape {
   static constexpr int segw = kThreads * px;
 };
 constexpr int kRows2D = 2;                   // K1c: target rows per step (2-D tables; 4: slower)
+constexpr int kColGroup = 4;                 // K1b: segments per column group (see colgroup_item)
 
 struct AxisEntry {   // one resolved column (or row) of one tile
   int32_t f;         // source index of floor(ix) (nearest: of rint(ix)); -1 = outside source
@@ -88,7 +89,7 @@ struct Geometry {
   int64_t band;   // target rows per work item of the gathers
   int64_t segw;   // target columns per work item (kThreads x columns per thread)
   int64_t band_first;   // bands of tile row ty0 above row_begin (not in the work list)
-  int64_t xgroup;       // consecutive bands an XCD takes in turn (K1b; 1 in the product)
+  int64_t colgroup;     // K1b: adjacent segments an XCD walks down together (kColGroup)
 };
 
 // numpy fancy index on a window axis of length `win` with an int16 index:
@@ -231,8 +232,9 @@ struct GatherArgs {
 };
 
 // Work decomposition shared by K1b/K1c: bands of kBand rows inside one tile row
-// x segments of kSegW columns inside one tile column, band-major; the XCDs
-// take whole bands in turn (xcd_groups, group = nsegs).  The list starts at
+// x segments of kSegW columns inside one tile column, band-major; K1c's XCDs
+// take whole bands in turn (xcd_groups, group = nsegs), K1b's walk column
+// groups (colgroup_item).  The list starts at
 // the band holding row_begin and ends at the band holding row_end - 1, so a
 // row band of the raster (a rank's share) has no empty items (blocks are dealt
 // to XCDs round-robin whatever their cost: empty items would idle an XCD).
@@ -258,6 +260,31 @@ __device__ inline bool work_item(const Geometry& g, int64_t w, int64_t ty0, int6
   return it.r0 < it.r1 && it.c0 < it.c1;
 }
 
+// K1b's deal.  Every item reads its segment's 512 x-table entries (16 B
+// each: 8 KB beside 64 KB of source taps).  Dealt band by band, an XCD met
+// the same segment again only one band later — about 10 MB of streamed taps
+// and stores through its 4 MB L2 — so every item fetched its entries from
+// memory again: 1/8 more read traffic (size-resolved request counters, an
+// identity launch reads 1.125x its bytes; profiles/r04_traffic*.json).  Here
+// the items are ordered by (column group of `G` adjacent segments, band,
+// segment in the group) and each XCD takes one contiguous eighth of that
+// list (blocks are dealt to the XCDs round-robin, block b -> b % 8): an XCD
+// walks down G adjacent segment columns band after band, so an x-table slice,
+// the source rows two bands share and the partial lines two adjacent segments
+// share are all reused from its L2 within a few items.  Returns the
+// band-major index work_item() decodes, or -1 past the list.
+__device__ inline int64_t colgroup_item(int64_t nwork, int64_t nsegs, int64_t G, int64_t idx) {
+  if (idx >= nwork) return -1;
+  const int64_t nbands = nwork / nsegs;
+  const int64_t gsize = nbands * G;          // items of a full group
+  const int64_t gi = idx / gsize;
+  const int64_t r = idx - gi * gsize;
+  const int64_t s0 = gi * G;
+  const int64_t gw = min(G, nsegs - s0);     // the last group may be narrower
+  const int64_t band = r / gw;
+  return band * nsegs + s0 + (r - band * gw);
+}
+
 // ---- K1b: separable gather --------------------------------------------------
 // No rows are carried between target rows: every target row loads its two
 // source rows (their overlap with the neighbouring rows is served by L1/L2),
@@ -269,9 +296,10 @@ gather_separable_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t bands_
   const Geometry& g = a.g;
   constexpr int kPx = K1Shape<O>::px, kRows = K1Shape<O>::rows;
   const T fill = Conv<T>::from_f64(a.fill);
-  for (XcdGroups sl = xcd_groups(nwork, nsegs * g.xgroup);; sl.i += sl.step) {
-    const int64_t w = sl.item();
-    if (w >= nwork) break;
+  const int64_t xcd = blockIdx.x & 7, per = (nwork + 7) / 8;
+  for (int64_t i = blockIdx.x >> 3; i < per; i += gridDim.x >> 3) {
+    const int64_t w = colgroup_item(nwork, nsegs, g.colgroup, xcd * per + i);
+    if (w < 0) break;
     WorkItem it;
     if (!work_item(g, w, ty0, nsegs, bands_per_tile, segs_per_tile, it)) continue;
     const AxisEntry* xt = a.xtab + it.t * g.tile_w + (it.c0 - it.tx * g.tile_w);
@@ -612,7 +640,7 @@ inline Work work_of(const GatherArgs& a, int64_t band = kBand, int64_t segw = kS
   const int64_t band_knob = xrs_testing_value(XRS_TESTING_REPROJECT_BAND);
   k.args.g.band = band_knob > 0 ? band_knob : band;
   const int64_t group_knob = xrs_testing_value(XRS_TESTING_REPROJECT_XCD_GROUP);
-  k.args.g.xgroup = group_knob > 0 ? group_knob : 1;
+  k.args.g.colgroup = group_knob > 0 ? group_knob : kColGroup;
   k.args.g.segw = segw;
   k.bands_per_tile = (g.tile_h + k.args.g.band - 1) / k.args.g.band;
   k.segs_per_tile = (g.tile_w + k.args.g.segw - 1) / k.args.g.segw;
@@ -769,7 +797,7 @@ extern "C" int xrs_reproject(const void* src, int src_dtype, int64_t n, int64_t 
   g.ntiles_y = (dst_h + tile_h - 1) / tile_h;
   g.src_x = src_x; g.src_y = src_y; g.tile_x0 = tile_x0; g.tile_y0 = tile_y0;
   g.tile_win = tile_win; g.win_h = win_h; g.win_w = win_w;
-  g.x_res = x_res; g.neg_y_res = -y_res; g.err_flags = err_flags; g.band = kBand; g.segw = kSegW; g.band_first = 0; g.xgroup = 1;
+  g.x_res = x_res; g.neg_y_res = -y_res; g.err_flags = err_flags; g.band = kBand; g.segw = kSegW; g.band_first = 0; g.colgroup = kColGroup;
   a.src = src; a.n = n; a.src_sn = src_sn; a.src_sy = src_sy;
   a.dst = dst; a.dst_sn = dst_sn; a.dst_sy = dst_sy; a.fill = fill;
   a.xtab = a.ytab = nullptr;
@@ -852,7 +880,7 @@ extern "C" int xrs_reproject_proj(const void* src, int src_dtype, int64_t n, int
   g.ntiles_y = (dst_h + tile_h - 1) / tile_h;
   g.src_x = grid_x; g.src_y = grid_y; g.tile_x0 = tile_x0; g.tile_y0 = tile_y0;
   g.tile_win = tile_win; g.win_h = win_h; g.win_w = win_w;
-  g.x_res = x_res; g.neg_y_res = -y_res; g.err_flags = err_flags; g.band = kBand; g.segw = kSegW; g.band_first = 0; g.xgroup = 1;
+  g.x_res = x_res; g.neg_y_res = -y_res; g.err_flags = err_flags; g.band = kBand; g.segw = kSegW; g.band_first = 0; g.colgroup = kColGroup;
   a.src = src; a.n = n; a.src_sn = src_sn; a.src_sy = src_sy;
   a.dst = dst; a.dst_sn = dst_sn; a.dst_sy = dst_sy; a.fill = fill;
   a.xtab = a.ytab = nullptr;
