@@ -329,8 +329,8 @@ int xrs_rectify_var(const double* ij, int64_t ij_sn, int64_t dst_h, int64_t dst_
  *                                         pixel floor by the exact division
  *   XRS_TESTING_RECTIFY_MARGIN            k > 1: K5 widens its float32 form margin
  *                                         k-fold (more pixels take the exact test)
- *   XRS_TESTING_REPROJECT_XCD_GROUP       k > 0: K1b's column groups are k
- *                                         segments wide (0 = 4)
+ *   XRS_TESTING_REPROJECT_XCD_GROUP       k > 0: K1b deals column groups of k
+ *                                         segments instead of whole bands (0)
  * Returns the previous value (or XRS_ERR_ARG for an unknown knob).
  * ------------------------------------------------------------------------- */
 #define XRS_TESTING_REPROJECT_BAND 1

@@ -42,11 +42,11 @@ def test_kernel_matches_reference_bitwise(case, interp):
                                             (8, 0, 4), (3, 1, 2), (4, 0, 1), (2, 0, 3),
                                             (1, 1, 5)])
 def test_work_shapes_are_bit_identical(band, bpc, group):
-    """K1's work decomposition (target rows per work item, grid cap, the width
-    of K1b's column groups) changes only which block computes a pixel: items
-    that split tiles (5 / 1 rows), a single block per CU (grid-stride loop),
-    column groups of 1-5 segments (a narrower last group) — all reproduce
-    the reference bit for bit.  The shapes are forced through the test-only knobs
+    """K1's work decomposition (target rows per work item, grid cap, K1b's
+    column-group deal instead of whole bands) changes only which block
+    computes a pixel: items that split tiles (5 / 1 rows), a single block per
+    CU (grid-stride loop), column groups of 1-5 segments (a narrower last
+    group) — all reproduce the reference bit for bit.  The shapes are forced through the test-only knobs
     (xrs_testing_set); the product never reads them from the environment."""
     import torch
 

@@ -65,7 +65,7 @@ struct K1Shape {
   static constexpr int segw = kThreads * px;
 };
 constexpr int kRows2D = 2;                   // K1c: target rows per step (2-D tables; 4: slower)
-constexpr int kColGroup = 4;                 // K1b: segments per column group (see colgroup_item)
+constexpr int kColGroup = 0;                 // K1b deal: 0 = band by band (see colgroup_item)
 
 struct AxisEntry {   // one resolved column (or row) of one tile
   int32_t f;         // source index of floor(ix) (nearest: of rint(ix)); -1 = outside source
@@ -89,7 +89,8 @@ struct Geometry {
   int64_t band;   // target rows per work item of the gathers
   int64_t segw;   // target columns per work item (kThreads x columns per thread)
   int64_t band_first;   // bands of tile row ty0 above row_begin (not in the work list)
-  int64_t colgroup;     // K1b: adjacent segments an XCD walks down together (kColGroup)
+  int64_t colgroup;     // K1b: 0 = bands dealt to the XCDs in turn (product); k > 0 =
+                        // column groups of k segments (colgroup_item; test knob)
 };
 
 // numpy fancy index on a window axis of length `win` with an int16 index:
@@ -261,18 +262,25 @@ __device__ inline bool work_item(const Geometry& g, int64_t w, int64_t ty0, int6
 }
 
 // K1b's deal.  Every item reads its segment's 512 x-table entries (16 B
-// each: 8 KB beside 64 KB of source taps).  Dealt band by band, an XCD met
-// the same segment again only one band later — about 10 MB of streamed taps
-// and stores through its 4 MB L2 — so every item fetched its entries from
-// memory again: 1/8 more read traffic (size-resolved request counters, an
-// identity launch reads 1.125x its bytes; profiles/r04_traffic*.json).  Here
-// the items are ordered by (column group of `G` adjacent segments, band,
-// segment in the group) and each XCD takes one contiguous eighth of that
-// list (blocks are dealt to the XCDs round-robin, block b -> b % 8): an XCD
-// walks down G adjacent segment columns band after band, so an x-table slice,
-// the source rows two bands share and the partial lines two adjacent segments
-// share are all reused from its L2 within a few items.  Returns the
-// band-major index work_item() decodes, or -1 past the list.
+// each: 8 KB beside 64 KB of source taps).  Dealt band by band (the
+// product), an XCD meets the same segment again only one band later — about
+// 10 MB of streamed taps and stores through its 4 MB L2 — so every item
+// fetches its entries through the fabric again: an identity launch reads
+// 1.125x its bytes at the L2's memory side, the bench launch 1.154x
+// (size-resolved request counters, profiles/r04_k1_colgroup_ab.jsonl).  The
+// column-group deal below orders the items by (group of G adjacent
+// segments, band, segment in the group) and gives each XCD one contiguous
+// eighth: an XCD walks down G segment columns, so x-table slices, band seams
+// and segment seams come from its L2 (identity 1.004x, bench 1.043x) — and
+// K1 runs 2-15 % SLOWER (G = 1 / 2 / 4 / 8: 2.86-2.92 / 2.63-2.64 /
+// 2.59-2.79 / 2.51-2.53 ms against 2.46-2.49 ms band by band, interleaved on
+// one box).  The re-fetched slices are Infinity-Cache hits; what costs is
+// the DRAM pattern: band by band, the requests in flight sweep whole rows,
+// while narrow column groups scatter them over many rows (plain copies show
+// the same: the wider the address window in flight, the slower, 6.2 TB/s at
+// 4 KB per block down to 5.2 TB/s at 64 KB, scripts/xcd_probe.py).  Kept as
+// the XRS_TESTING_REPROJECT_XCD_GROUP alternative (bit-identical results).
+// Returns the band-major index work_item() decodes, or -1 past the list.
 __device__ inline int64_t colgroup_item(int64_t nwork, int64_t nsegs, int64_t G, int64_t idx) {
   if (idx >= nwork) return -1;
   const int64_t nbands = nwork / nsegs;
@@ -296,10 +304,19 @@ gather_separable_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t bands_
   const Geometry& g = a.g;
   constexpr int kPx = K1Shape<O>::px, kRows = K1Shape<O>::rows;
   const T fill = Conv<T>::from_f64(a.fill);
+  // the XCDs take whole bands in turn (XCD x: bands x, x + 8, ...); the
+  // column-group deal (colgroup_item) is the test knob's alternative
   const int64_t xcd = blockIdx.x & 7, per = (nwork + 7) / 8;
-  for (int64_t i = blockIdx.x >> 3; i < per; i += gridDim.x >> 3) {
-    const int64_t w = colgroup_item(nwork, nsegs, g.colgroup, xcd * per + i);
-    if (w < 0) break;
+  for (int64_t i = blockIdx.x >> 3;; i += gridDim.x >> 3) {
+    int64_t w;
+    if (g.colgroup > 0) {
+      w = i < per ? colgroup_item(nwork, nsegs, g.colgroup, xcd * per + i) : -1;
+      if (w < 0) break;
+    } else {
+      const int64_t m = i / nsegs;
+      w = (m * 8 + xcd) * nsegs + (i - m * nsegs);
+      if (w >= nwork) break;
+    }
     WorkItem it;
     if (!work_item(g, w, ty0, nsegs, bands_per_tile, segs_per_tile, it)) continue;
     const AxisEntry* xt = a.xtab + it.t * g.tile_w + (it.c0 - it.tx * g.tile_w);
