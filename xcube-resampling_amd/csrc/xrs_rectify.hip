@@ -172,22 +172,45 @@ ij_bboxes_kernel(BBoxArgs a, int64_t chunk) {
     xn = a.x[(int64_t)j * a.sy + (idx - j * w32)];
     yn = a.y[(int64_t)j * a.sy + (idx - j * w32)];
   }
+  // the lane's pixel as (row, column), stepped by kThreads pixels per
+  // iteration without a division (i < w kept by subtracting whole rows)
+  int32_t ci = 0, cj = 0;
+  {
+    const uint32_t idx = (uint32_t)min(p0 + (int64_t)threadIdx.x, n - 1);
+    cj = (int32_t)(idx / w32);
+    ci = (int32_t)(idx - (uint32_t)cj * w32);
+  }
+  auto step = [&](int32_t& i, int32_t& j) {
+    i += kThreads;
+    while (i >= (int32_t)w32) { i -= (int32_t)w32; ++j; }
+  };
+  // Wave accumulator (grid mode): the box every contributing lane of the
+  // wave's recent iterations fell in, and its extremes so far — flushed to
+  // the block's accumulators only when the wave meets another box (lanes
+  // cross a tile every few hundred pixels) instead of four atomics per
+  // iteration.  Wave-uniform values (scalar registers).
+  int32_t wk = -1, wimin = INT32_MAX, wjmin = INT32_MAX, wimax = -1, wjmax = -1;
+  auto wflush = [&]() {
+    if (wk >= 0 && (threadIdx.x & 63) == 0) {
+      atomicMin(&acc[4 * wk + 0], wimin);
+      atomicMin(&acc[4 * wk + 1], wjmin);
+      atomicMax(&acc[4 * wk + 2], wimax);
+      atomicMax(&acc[4 * wk + 3], wjmax);
+    }
+    wk = -1;
+  };
   // every lane of a wave iterates the same number of times (wave-uniform trip
   // count), so the wave-wide shuffles below always see all 64 lanes
   for (int64_t base = p0; base < p1; base += kThreads) {
     const int64_t idx = base + threadIdx.x;
     const bool valid = idx < p1;
     const double x = xn, y = yn;
-    int32_t i0 = 0, j0 = 0;
-    if (valid) {
-      j0 = (int32_t)((uint32_t)idx / w32);
-      i0 = (int32_t)((uint32_t)idx - (uint32_t)j0 * w32);
-    }
+    const int32_t i0 = valid ? ci : 0, j0 = valid ? cj : 0;
+    step(ci, cj);
     if (idx + kThreads < p1) {
-      const uint32_t nidx = (uint32_t)(idx + kThreads);
-      const uint32_t j = nidx / w32;
-      xn = a.x[(int64_t)j * a.sy + (nidx - j * w32)];
-      yn = a.y[(int64_t)j * a.sy + (nidx - j * w32)];
+      const int64_t o = (int64_t)cj * a.sy + ci;
+      xn = a.x[o];
+      yn = a.y[o];
     }
     int32_t tx0 = 1, tx1 = 0, ty0 = 1, ty1 = 0;
     if (valid && a.ntx > 0) {  // x_min <= x <= x_max, y_min <= y <= y_max (bboxes.py:60-69)
@@ -202,6 +225,43 @@ ij_bboxes_kernel(BBoxArgs a, int64_t chunk) {
       } else {
         for (int32_t t = 0; t < (int32_t)a.nty; ++t)
           if (by[2 * t] <= y && y <= by[2 * t + 1]) { if (ty0 > ty1) ty0 = t; ty1 = t; }
+      }
+    }
+    if (a.ntx > 0) {
+      // one box per pixel for every lane that has one, the same box: the
+      // wave accumulator takes the iteration (lanes are consecutive pixels:
+      // when the first and the last contributing lane share a row, the
+      // extremes are theirs)
+      const bool any_box = valid && tx0 <= tx1 && ty0 <= ty1;
+      const bool single = any_box && tx0 == tx1 && ty0 == ty1;
+      const int32_t kl = single ? ty0 * (int32_t)a.ntx + tx0 : (any_box ? -2 : INT32_MAX);
+      const uint64_t has = __ballot(kl != INT32_MAX);
+      if (has == 0) continue;
+      const int fl = __builtin_ctzll(has), ll = 63 - __builtin_clzll(has);
+      const int32_t k0 = __builtin_amdgcn_readlane(kl, fl);
+      if (k0 >= 0 && __all(kl == k0 || kl == INT32_MAX)) {
+        int32_t imin, jmin, imax, jmax;
+        const int32_t jf = __builtin_amdgcn_readlane(j0, fl);
+        if (__builtin_amdgcn_readlane(j0, ll) == jf) {
+          imin = __builtin_amdgcn_readlane(i0, fl);
+          imax = __builtin_amdgcn_readlane(i0, ll);
+          jmin = jmax = jf;
+        } else {
+          const bool mine = kl == k0;
+          imin = wave_min(mine ? i0 : INT32_MAX);
+          jmin = wave_min(mine ? j0 : INT32_MAX);
+          imax = wave_max(mine ? i0 : -1);
+          jmax = wave_max(mine ? j0 : -1);
+        }
+        if (k0 != wk) {
+          wflush();
+          wk = k0;
+          wimin = imin; wjmin = jmin; wimax = imax; wjmax = jmax;
+        } else {
+          wimin = min(wimin, imin); wjmin = min(wjmin, jmin);
+          wimax = max(wimax, imax); wjmax = max(wjmax, jmax);
+        }
+        continue;
       }
     }
     int32_t cur = valid ? next_box(a, bx, x, y, tx0, tx1, ty0, ty1, -1) : INT32_MAX;
@@ -239,6 +299,7 @@ ij_bboxes_kernel(BBoxArgs a, int64_t chunk) {
       if (mine) cur = next_box(a, bx, x, y, tx0, tx1, ty0, ty1, k);
     }
   }
+  wflush();
   if (SHARED) {
     __syncthreads();
     for (int64_t k = threadIdx.x; k < a.nboxes; k += kThreads) {
@@ -291,6 +352,8 @@ struct RectArgs {
   float margin_scale;          // form margin factor (tests: >1 widens the exact-test band)
   int narrow;                  // dst_h * dst_w < 2^30, dst_w < 2^24: claims use 32-bit byte
                                // offsets and 24-bit multiplies
+  int tri_bit;                 // h * w < 2^31: a claim key is (raster key << 1) | (the
+                               // reference's triangle is B), so K5b evaluates one triangle
   uint32_t* keys;              // (dst_h, dst_w) claim keys, 0xFFFFFFFF = free
   double* ij;                  // (2, dst_h, dst_w) output
   int32_t* err_flags;          // XRS_EFLAG_STATE: an inconsistent record / key was skipped
@@ -342,6 +405,23 @@ __device__ inline int quad_hit(const RectArgs& a, const Quad& q, double dx, doub
     }
   }
   return 0;
+}
+
+// The clamped (u, v) of ONE triangle (A = (p0; p2, p1), B = (p3; p1, p2)) at
+// pixel centre (dx, dy), with the reference's expressions and divisions
+// (rectify.py:556-573, 737-768): origin O, fu's edge corner U, fv's corner V
+// = (p0, p2, p1) or (p3, p1, p2); det = _fdet(O, V, U).  The claim picked the
+// triangle (claim keys carry it), so the triangle hits here.
+__device__ inline void tri_uv(const Quad& q, bool b, double dx, double dy, double& cu,
+                              double& cv) {
+  const double ox = b ? q.x3 : q.x0, oy = b ? q.y3 : q.y0;
+  const double ux = b ? q.x1 : q.x2, uy = b ? q.y1 : q.y2;
+  const double vx = b ? q.x2 : q.x1, vy = b ? q.y2 : q.y1;
+  const double det = fdet(ox, oy, vx, vy, ux, uy);
+  const double u = fu(dx, dy, ox, oy, ux, uy) / det;
+  const double v = fv(dx, dy, ox, oy, vx, vy) / det;
+  cu = fclamp(u, 0.0, 1.0);
+  cv = fclamp(v, 0.0, 1.0);
 }
 
 __device__ inline void quad_dets(const Quad& q, double& det_a, double& det_b) {
@@ -485,6 +565,19 @@ __device__ inline bool tri_exact(const Quad& q, bool tri_b, double dx, double dy
   return u >= umin && v >= umin && u + v <= uvmax;
 }
 
+// The reference's triangle for pixel centre (dx, dy): 1 = A hits, 2 = A
+// misses and B hits, 0 = neither (rectify.py:556-573: A is tested first)
+__device__ inline int tri_choice_exact(const Quad& q, double dx, double dy, double umin,
+                                       double uvmax) {
+  if (tri_exact(q, false, dx, dy, umin, uvmax)) return 1;
+  return tri_exact(q, true, dx, dy, umin, uvmax) ? 2 : 0;
+}
+
+// The claim key of quad `key` for a pixel won by triangle `tri` (1 / 2).
+__device__ inline uint32_t claim_key(const RectArgs& a, uint32_t key, int tri) {
+  return a.tri_bit ? (key << 1) | (uint32_t)(tri - 1) : key;
+}
+
 // One triangle's forms for the pair walk: 1 = forms set up, 0 = no triangle
 // (_fdet NaN or 0: never hits; forms that are -inf everywhere), -1 = no usable
 // bound (the lane takes the reference's test over the untrimmed window).
@@ -516,10 +609,12 @@ __device__ inline f32x2 form2(float a0, float ai, float aj, float b0, float bi, 
 
 // Walk the window's n pixels (row-major, nw per row) for both triangles at
 // once: triangle A in the low and B in the high half of packed float32 FMAs
-// (v_pk_fma_f32).  Returns (hit, undecided) bit masks: hit when some
-// triangle's min3 >= 0, undecided when neither hits and some min3 >= -2M.
-__device__ inline uint2 walk_pair(const TriForms A, const TriForms B, int n, int nw) {
-  uint32_t h_hit = 0, h_uns = 0;
+// (v_pk_fma_f32).  Returns bit masks (hit by A, hit by B, undecided): the
+// reference tests A first, so a pixel is A's when A surely hits (min3 >= 0),
+// B's when B surely hits and A surely misses (min3 < -2M); any other pixel
+// with some min3 >= -2M takes the exact tests.
+__device__ inline uint3 walk_pair(const TriForms A, const TriForms B, int n, int nw) {
+  uint32_t h_a = 0, h_b = 0, h_uns = 0;
   float af = 0.0f, bf = 0.0f;
   int col = 0;
   for (int k = 0; k < n; ++k) {
@@ -529,12 +624,14 @@ __device__ inline uint2 walk_pair(const TriForms A, const TriForms B, int n, int
     const f32x2 w = form2(A.w0, A.wi, A.wj, B.w0, B.wi, B.wj, av, bv);
     const float ha = fminf(u.x, fminf(v.x, w.x)), hb = fminf(u.y, fminf(v.y, w.y));
     const uint32_t bit = 1u << k;
-    h_hit |= fmaxf(ha, hb) >= 0.0f ? bit : 0u;
-    h_uns |= (ha >= A.thr || hb >= B.thr) ? bit : 0u;
+    const bool a_in = ha >= 0.0f, a_near = ha >= A.thr;
+    h_a |= a_in ? bit : 0u;
+    h_b |= (hb >= 0.0f && !a_near) ? bit : 0u;
+    h_uns |= (a_near || hb >= B.thr) ? bit : 0u;
     af += 1.0f;
     if (++col == nw) { col = 0; af = 0.0f; bf += 1.0f; }
   }
-  return uint2{h_hit, h_uns};
+  return uint3{h_a, h_b, h_uns & ~(h_a | h_b)};
 }
 
 // Trim a quad's window [i0, i1] x [j0, j1] (floors of the corners' extreme
@@ -631,8 +728,8 @@ __device__ inline void claim_exact_lane(const RectArgs& a, const TileInfo& ti, i
     const double dy = ti.y_off + ((double)dj + 0.5) * a.y_scale;
     for (int32_t di = (int32_t)i0; di <= (int32_t)i1; ++di) {
       const double dx = ti.x_off + ((double)di + 0.5) * a.x_scale;
-      if (tri_exact(Q, false, dx, dy, umin, uvmax) || tri_exact(Q, true, dx, dy, umin, uvmax))
-        atomicMin(a.keys + (int64_t)(ti.r0 + dj) * a.dst_w + ti.c0 + di, key);
+      const int tri = tri_choice_exact(Q, dx, dy, umin, uvmax);
+      if (tri) atomicMin(a.keys + (int64_t)(ti.r0 + dj) * a.dst_w + ti.c0 + di, claim_key(a, key, tri));
     }
   }
 }
@@ -712,7 +809,8 @@ rectify_claim_kernel(RectArgs a) {
       int32_t imin = 0, jmin = 0, nw = 0;
       int64_t big_cnt = 0;   // > 0: window above kLaneWindow, walked by the wave below
       bool slow = false;     // window not decided fast: claim_exact_lane
-      uint32_t hit = 0, unsure = 0;   // bit k: window pixel k (row-major) hit / undecided
+      uint32_t hit = 0, hit_b = 0, unsure = 0;   // bit k: window pixel k (row-major) hit
+                                                  // (hit_b: by triangle B) / undecided
       if (has_q) {
         double fx0, fx1, fy0, fy1;
         // floor is monotone and the reciprocal's error tiny: the extremes of the
@@ -766,9 +864,10 @@ rectify_claim_kernel(RectArgs a) {
               if (sa < 0 || sb < 0) {
                 slow = true;   // a triangle without a usable bound: exact, untrimmed window
               } else if (sa | sb) {
-                const uint2 m = walk_pair(FA, FB, n, nw);
-                hit = m.x;
-                unsure = m.y & ~hit;
+                const uint3 m = walk_pair(FA, FB, n, nw);
+                hit = m.x | m.y;
+                hit_b = m.y;
+                unsure = m.z;
               }
             }
           }
@@ -777,6 +876,8 @@ rectify_claim_kernel(RectArgs a) {
         }
       }
       const uint32_t key = (uint32_t)qj * (uint32_t)a.w + (uint32_t)qi;
+      // claim keys of the two triangles (tri_bit: the low bit names B)
+      const uint32_t key_a = claim_key(a, key, 1), key_b = claim_key(a, key, 2);
       // claims: the window pixels hit (row k / nw, column k % nw: exact in float
       // for k < 16, the quotient is >= 1/32 from an integer)
       if (hit | unsure) {
@@ -794,14 +895,15 @@ rectify_claim_kernel(RectArgs a) {
             const uint32_t dj = (uint32_t)(((float)k + 0.5f) * rnw);
             const uint32_t off = lbase + (uint32_t)k + __umul24(dj, lstride);
             atomicMin(reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(tile_keys) + (off << 2)),
-                      key);
+                      (hit_b >> k) & 1u ? key_b : key_a);
           }
         }
         while (hit) {
           const int k = __builtin_ctz(hit);
           hit &= hit - 1;
           const int32_t dj = (int32_t)(((float)k + 0.5f) * rnw);
-          atomicMin(tile_keys + (int64_t)(jmin + dj) * a.dst_w + imin + k - dj * nw, key);
+          atomicMin(tile_keys + (int64_t)(jmin + dj) * a.dst_w + imin + k - dj * nw,
+                    (hit_b >> k) & 1u ? key_b : key_a);
         }
         if (unsure) {   // a pixel centre within the margin of an edge: the reference's test
           const Quad Q = load_quad(a, qj, qi);
@@ -812,8 +914,9 @@ rectify_claim_kernel(RectArgs a) {
             const int32_t di = imin + k - dj * nw;
             const double dy = ti.y_off + ((double)(jmin + dj) + 0.5) * a.y_scale;
             const double dx = ti.x_off + ((double)di + 0.5) * a.x_scale;
-            if (tri_exact(Q, false, dx, dy, umin, uvmax) || tri_exact(Q, true, dx, dy, umin, uvmax))
-              atomicMin(tile_keys + (int64_t)(jmin + dj) * a.dst_w + di, key);
+            const int tri = tri_choice_exact(Q, dx, dy, umin, uvmax);
+            if (tri)
+              atomicMin(tile_keys + (int64_t)(jmin + dj) * a.dst_w + di, tri == 1 ? key_a : key_b);
           } while (unsure);
         }
       }
@@ -828,7 +931,8 @@ rectify_claim_kernel(RectArgs a) {
         const int32_t wi0 = __builtin_amdgcn_readlane(imin, o);
         const int32_t wj0 = __builtin_amdgcn_readlane(jmin, o);
         const int32_t wnw = __builtin_amdgcn_readlane(nw, o);
-        const uint32_t wkey = __builtin_amdgcn_readlane(key, o);
+        const uint32_t wkey_a = __builtin_amdgcn_readlane(key_a, o);
+        const uint32_t wkey_b = __builtin_amdgcn_readlane(key_b, o);
         const int64_t wcnt =
             ((int64_t)__builtin_amdgcn_readlane((uint32_t)(big_cnt >> 32), o) << 32) |
             __builtin_amdgcn_readlane((uint32_t)big_cnt, o);
@@ -839,8 +943,10 @@ rectify_claim_kernel(RectArgs a) {
         for (int64_t k = lane; k < wcnt; k += 64) {
           const double dy = ti.y_off + ((double)(wj0 + dj) + 0.5) * a.y_scale;
           const double dx = ti.x_off + ((double)(wi0 + di) + 0.5) * a.x_scale;
-          if (tri_exact(Q, false, dx, dy, umin, uvmax) || tri_exact(Q, true, dx, dy, umin, uvmax))
-            atomicMin(a.keys + (int64_t)(ti.r0 + wj0 + dj) * a.dst_w + ti.c0 + wi0 + di, wkey);
+          const int tri = tri_choice_exact(Q, dx, dy, umin, uvmax);
+          if (tri)
+            atomicMin(a.keys + (int64_t)(ti.r0 + wj0 + dj) * a.dst_w + ti.c0 + wi0 + di,
+                      tri == 1 ? wkey_a : wkey_b);
           dj += step_r;
           di += step_c;
           if (di >= wnw) { di -= wnw; ++dj; }
@@ -1049,9 +1155,15 @@ rectify_resolve_kernel(RectArgs a, FusedVar fv) {
         key[r] = r < nr ? a.keys[p0 + r * a.dst_w] : 0xFFFFFFFFu;
       Quad Q[kResolveRows];
       int64_t qj[kResolveRows], qi[kResolveRows];
+      bool tri_b[kResolveRows];   // tri_bit: the claim found the reference's triangle B
 #pragma unroll
       for (int r = 0; r < kResolveRows; ++r) {
+        tri_b[r] = false;
         if (key[r] != 0xFFFFFFFFu) {
+          if (a.tri_bit) {
+            tri_b[r] = (key[r] & 1u) != 0;
+            key[r] >>= 1;
+          }
           // key / w through the reciprocal, corrected to the exact quotient
           int64_t j = (int64_t)((double)key[r] * inv_w);
           int64_t i = (int64_t)key[r] - j * a.w;
@@ -1075,13 +1187,21 @@ rectify_resolve_kernel(RectArgs a, FusedVar fv) {
         if (r >= nr) break;
         double oi = NAN, oj = NAN;
         if (key[r] != 0xFFFFFFFFu) {
-          double det_a, det_b;
-          quad_dets(Q[r], det_a, det_b);
           const int32_t dj = rb + r;
           const double dy = ti.y_off + ((double)dj + 0.5) * a.y_scale;
           const double dx = ti.x_off + ((double)di + 0.5) * a.x_scale;
           double cu, cv;
-          const int tri = quad_hit(a, Q[r], dx, dy, det_a, det_b, cu, cv);
+          int tri;
+          if (a.tri_bit) {
+            // the claim decided the reference's triangle: evaluate that one
+            // only (rectify.py:556-573), its corners chosen by selects
+            tri = tri_b[r] ? 2 : 1;
+            tri_uv(Q[r], tri_b[r], dx, dy, cu, cv);
+          } else {
+            double det_a, det_b;
+            quad_dets(Q[r], det_a, det_b);
+            tri = quad_hit(a, Q[r], dx, dy, det_a, det_b, cu, cv);
+          }
           if (tri) {
             const int64_t li = qi[r] - ti.si0, lj = qj[r] - ti.sj0;   // tile-local quad
             double src_i, src_j;
@@ -1260,6 +1380,7 @@ int rectify_ij_impl(const char* what, const double* x, const double* y, int64_t 
   const int64_t widen = xrs_testing_value(XRS_TESTING_RECTIFY_MARGIN);
   a.margin_scale = widen > 1 ? (float)widen : 1.0f;
   a.narrow = (dst_h * dst_w < ((int64_t)1 << 30) && dst_w < ((int64_t)1 << 24)) ? 1 : 0;
+  a.tri_bit = h * w < ((int64_t)1 << 31) ? 1 : 0;
   XRS_HIP_CHECK(hipMemsetAsync(keys, 0xFF, (size_t)(dst_h * dst_w) * sizeof(uint32_t), st));
   {
     // as many blocks as are resident at once (fewer when the caller knows a
