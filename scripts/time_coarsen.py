@@ -1,0 +1,49 @@
+"""Config-3 coarsen (16384^2 f32 -> 4096^2, 4x4 mean through the affine path)
+timed in isolation for A/B arms of the K3i kernel: K launches replayed from a
+captured graph after a warm-up; prints 'ms per launch'.  The corner block is
+checked against the product's output first (arms must be bit-identical).
+    XRS_LIBRARY=probe/ARM/pkg/lib/libxrs.so python scripts/time_coarsen.py"""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "scripts"))
+
+
+def main():
+    import torch
+
+    import bench_configs as bc
+    import xcube_resampling_amd as xrs
+    import xcube_resampling_amd.affine as A
+    from xcube_resampling_amd import kernels
+
+    n, k = 16384, 4
+    res = 2.0 ** -10
+    lon = (np.arange(n) + 0.5) * res
+    lat = n * res - (np.arange(n) + 0.5) * res
+    sgm = xrs.GridMapping.from_coords(xrs.DataArray(lon, "lon", name="lon"),
+                                      xrs.DataArray(lat, "lat", name="lat"), "EPSG:4326")
+    tgm = xrs.GridMapping.regular((n // k, n // k), (0, 0), res * k, "EPSG:4326")
+    m = tgm.ij_transform_to(sgm)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(20250905)
+    src = torch.rand((1, n, n), generator=g, device="cuda", dtype=torch.float32)
+    oc = (1, tgm.tile_height, tgm.tile_width)
+    plan = A.plan_affine(tuple(src.shape), np.dtype(np.float32), m, (1, n // k, n // k), oc, 1,
+                         "mean", False, np.nan)
+    out = kernels.affine(src, plan)
+    ref = src[0].reshape(n // k, k, n // k, k).mean(dim=(1, 3))
+    # interior pixels: the 4x4 mean (numpy pairwise order differs from torch's:
+    # compare with a tolerance here; the GPU suite checks bit-exactness)
+    assert torch.allclose(out[0, :-1, :-1], ref[:-1, :-1], rtol=1e-6, atol=1e-6)
+    ms, wall = bc._timed(lambda: kernels.affine(src, plan, out), 20, 5, graph=True)
+    print(f"{os.environ.get('XRS_LIBRARY', 'product')}: {ms:.4f} ms per launch "
+          f"({(4 * n * n + 4 * (n // k) ** 2) / (ms / 1e3) / 1e9:.0f} GB/s)", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -25,6 +25,7 @@
 
 #include <cmath>
 #include <cstdlib>
+#include <type_traits>
 
 #include "xrs_common.hpp"
 
@@ -1127,7 +1128,7 @@ __device__ inline void sample_rows(const double* fi, const double* fj, int nr,
   }
 }
 
-template <typename T, bool FUSE, int INTERP>
+template <typename T, bool FUSE, int INTERP, bool TRI>   // TRI: a.tri_bit (compile time)
 __global__ void __launch_bounds__(kThreads)
 rectify_resolve_kernel(RectArgs a, FusedVar fv) {
   const int64_t n = a.dst_h * a.dst_w;
@@ -1147,12 +1148,11 @@ rectify_resolve_kernel(RectArgs a, FusedVar fv) {
     }
     if (rb >= ti.th) continue;
     const int32_t nr = min(kResolveRows, ti.th - rb);
-    for (int32_t di = threadIdx.x; di < ti.tw; di += kThreads) {
+    // a thread's columns di, di + kThreads of the item in pairs: the second
+    // column's keys are requested with the first's, so their round trip is
+    // hidden behind the first column's quads and arithmetic
+    auto column = [&](int32_t di, uint32_t (&key)[kResolveRows]) {
       const int64_t p0 = (int64_t)(ti.r0 + rb) * a.dst_w + ti.c0 + di;
-      uint32_t key[kResolveRows];
-#pragma unroll
-      for (int r = 0; r < kResolveRows; ++r)
-        key[r] = r < nr ? a.keys[p0 + r * a.dst_w] : 0xFFFFFFFFu;
       Quad Q[kResolveRows];
       int64_t qj[kResolveRows], qi[kResolveRows];
       bool tri_b[kResolveRows];   // tri_bit: the claim found the reference's triangle B
@@ -1160,7 +1160,7 @@ rectify_resolve_kernel(RectArgs a, FusedVar fv) {
       for (int r = 0; r < kResolveRows; ++r) {
         tri_b[r] = false;
         if (key[r] != 0xFFFFFFFFu) {
-          if (a.tri_bit) {
+          if (TRI) {
             tri_b[r] = (key[r] & 1u) != 0;
             key[r] >>= 1;
           }
@@ -1192,7 +1192,7 @@ rectify_resolve_kernel(RectArgs a, FusedVar fv) {
           const double dx = ti.x_off + ((double)di + 0.5) * a.x_scale;
           double cu, cv;
           int tri;
-          if (a.tri_bit) {
+          if (TRI) {
             // the claim decided the reference's triangle: evaluate that one
             // only (rectify.py:556-573), its corners chosen by selects
             tri = tri_b[r] ? 2 : 1;
@@ -1231,6 +1231,19 @@ rectify_resolve_kernel(RectArgs a, FusedVar fv) {
         sample_rows<T, INTERP, kResolveRows>(fi, fj, nr, fv, src, dst, p0, a.dst_w, tfill,
                                              bad);
       }
+    };
+    for (int32_t d0 = threadIdx.x; d0 < ti.tw; d0 += 2 * kThreads) {
+      const int32_t d1 = d0 + kThreads;
+      const bool has1 = d1 < ti.tw;
+      const int64_t q0 = (int64_t)(ti.r0 + rb) * a.dst_w + ti.c0 + d0;
+      uint32_t key0[kResolveRows], key1[kResolveRows];
+#pragma unroll
+      for (int r = 0; r < kResolveRows; ++r) {
+        key0[r] = r < nr ? a.keys[q0 + r * a.dst_w] : 0xFFFFFFFFu;
+        key1[r] = r < nr && has1 ? a.keys[q0 + kThreads + r * a.dst_w] : 0xFFFFFFFFu;
+      }
+      column(d0, key0);
+      if (has1) column(d1, key1);
     }
   }
   if (bad) atomicOr(a.err_flags, XRS_EFLAG_STATE);
@@ -1398,23 +1411,29 @@ int rectify_ij_impl(const char* what, const double* x, const double* y, int64_t 
     XRS_HIP_CHECK(hipGetLastError());
   }
   const int nb2 = grid_blocks(256 * 32, 1, 1 << 24);
-  if (!fv) {
-    hipLaunchKernelGGL((rectify_resolve_kernel<uint8_t, false, XRS_INTERP_NEAREST>), dim3(nb2),
-                       dim3(kThreads), 0, st, a, FusedVar{});
-  } else {
-    const int rc = dispatch_dtype(fv_dtype, [&](auto tag) -> int {
+  auto resolve = [&](auto tri) -> int {
+    constexpr bool TRI = decltype(tri)::value;
+    if (!fv) {
+      hipLaunchKernelGGL((rectify_resolve_kernel<uint8_t, false, XRS_INTERP_NEAREST, TRI>),
+                         dim3(nb2), dim3(kThreads), 0, st, a, FusedVar{});
+      return XRS_OK;
+    }
+    return dispatch_dtype(fv_dtype, [&](auto tag) -> int {
       using T = decltype(tag);
       if (fv->interp == XRS_INTERP_NEAREST)
-        hipLaunchKernelGGL((rectify_resolve_kernel<T, true, XRS_INTERP_NEAREST>), dim3(nb2),
+        hipLaunchKernelGGL((rectify_resolve_kernel<T, true, XRS_INTERP_NEAREST, TRI>), dim3(nb2),
                            dim3(kThreads), 0, st, a, *fv);
       else if (fv->interp == XRS_INTERP_TRIANGULAR)
-        hipLaunchKernelGGL((rectify_resolve_kernel<T, true, XRS_INTERP_TRIANGULAR>), dim3(nb2),
-                           dim3(kThreads), 0, st, a, *fv);
+        hipLaunchKernelGGL((rectify_resolve_kernel<T, true, XRS_INTERP_TRIANGULAR, TRI>),
+                           dim3(nb2), dim3(kThreads), 0, st, a, *fv);
       else
-        hipLaunchKernelGGL((rectify_resolve_kernel<T, true, XRS_INTERP_BILINEAR>), dim3(nb2),
-                           dim3(kThreads), 0, st, a, *fv);
+        hipLaunchKernelGGL((rectify_resolve_kernel<T, true, XRS_INTERP_BILINEAR, TRI>),
+                           dim3(nb2), dim3(kThreads), 0, st, a, *fv);
       return XRS_OK;
     });
+  };
+  {
+    const int rc = a.tri_bit ? resolve(std::true_type{}) : resolve(std::false_type{});
     if (rc != XRS_OK) {
       xrs_set_error("%s: unsupported variable dtype %d", what, fv_dtype);
       return XRS_ERR_ARG;
