@@ -587,11 +587,12 @@ affine_reduce_kernel(AffineArgs a, const AxisTab* __restrict__ ytab,
 // through the exact per-sub-sample path — same result, slower.  A list
 // longer than the workspace holds hands the whole launch to the generic K3.
 // output rows per item: 16 (f32) / 8 (f64) sub-sample rows of D elements,
-// 32 for f32 at D = 4 (R = 8 at config 3: 33 rows in flight per lane, 0.247
-// -> 0.240 ms vs R = 4; larger R elsewhere leaves loops rolled (scratch) or
-// one wave per SIMD)
+// 8 for f32 at D = 4.  Config 3 (round 4, items dealt to the XCDs band by
+// band): R = 2 (9 source rows per item) 0.213-0.214 ms against R = 8 (33
+// rows, 211 VGPRs, two waves per SIMD) 0.222 ms and R = 1 / 4 0.24 ms
+// (profiles/r04_k3_ab.log); round 3's XCD-slice deal had preferred R = 8.
 inline constexpr int64_t int_rows(int64_t d, int64_t esz) {
-  return d >= 8 ? 1 : (d == 4 && esz == 4) ? 8 : (16 / d) / (esz / 4) < 1 ? 1 : (16 / d) / (esz / 4);
+  return d >= 8 ? 1 : (d == 4 && esz == 4) ? 2 : (16 / d) / (esz / 4) < 1 ? 1 : (16 / d) / (esz / 4);
 }
 template <typename T, int D> struct IntItem {
   static constexpr int R = (int)int_rows(D, sizeof(T));
@@ -625,8 +626,15 @@ affine_reduce_integral_kernel(AffineArgs a, const int32_t* __restrict__ yrun,
   const int64_t ntx = (a.out_w + kThreads - 1) / kThreads;
   const int64_t nty = (a.out_h + R - 1) / R;
   const int64_t nwork = ntx * nty * a.nt;
-  const XcdSlice sl = xcd_slice(nwork);
-  for (int64_t w = sl.first; w < sl.end; w += sl.step) {
+  // the XCDs take whole bands of items in turn (XCD x: bands x, x + 8, ...):
+  // the chip's items in flight cover one contiguous run of source rows, and
+  // the row two bands share is read by neighbouring XCDs at about the same
+  // time.  Dealing each XCD one contiguous eighth of the image instead (eight
+  // separate runs in flight) took 0.231 vs 0.222 ms at config 3, items dealt
+  // one by one 0.261 ms (profiles/r04_k3_ab.log).
+  for (XcdGroups sg = xcd_groups(nwork, ntx);; sg.i += sg.step) {
+    const int64_t w = sg.item();
+    if (w >= nwork) break;
     const int64_t t = w / (ntx * nty);
     const int64_t rem = w - t * ntx * nty;
     const int64_t tj = rem / ntx, ti = rem - tj * ntx;
@@ -669,11 +677,20 @@ affine_reduce_integral_kernel(AffineArgs a, const int32_t* __restrict__ yrun,
         const int32_t rr = min(gf + r, (int32_t)(a.src_h - 1));
         const T* row = g0 + (int64_t)rr * a.src_sy;
         load_run<T, D>(row + cl, v[r]);
-        if (ORDER == 1) nbv[r] = row[cnb];
         if constexpr (T1) {
           const T* row1 = g1 + (int64_t)rr * a.src_sy;
           load_run<T, D>(row1 + cl, v1[r]);
           nbv1[r] = row1[cnb];
+        }
+      }
+      // the right-hand taps: from the next lane's run (shuffle below), loaded
+      // only by lanes whose neighbour does not hold it (a wave's last lane,
+      // a break in the runs) — one branch around all rows' loads
+      if (ORDER == 1 && !nb_lane) {
+#pragma unroll
+        for (int r = 0; r < NRT; ++r) {
+          const int32_t rr = min(gf + r, (int32_t)(a.src_h - 1));
+          nbv[r] = g0[(int64_t)rr * a.src_sy + cnb];
         }
       }
       if (ORDER == 1) {
