@@ -978,8 +978,10 @@ __device__ inline void sample_px(double fi, double fj, const T* __restrict__ src
     for (int64_t s = 0; s < n; ++s) dst[s * dst_sn + p] = tfill;
     return;
   }
-  int64_t i0 = (int64_t)fi, j0 = (int64_t)fj;   // int() truncation (values >= 0)
-  const double u = fi - (double)i0, v = fj - (double)j0;
+  // int() truncation of values in [0, src_w) / [0, src_h), both < 2^31
+  // (checked at launch): 32-bit conversions
+  int64_t i0 = (int32_t)fi, j0 = (int32_t)fj;
+  const double u = fi - (double)(int32_t)i0, v = fj - (double)(int32_t)j0;
   const int64_t imax = src_w - 1, jmax = src_h - 1;
   if (INTERP == XRS_INTERP_NEAREST) {
     if (u > 0.5) i0 = min(max(i0 + 1, (int64_t)0), imax);
@@ -1071,19 +1073,21 @@ __device__ inline void sample_rows(const double* fi, const double* fj, int nr,
       bad = true;
       continue;
     }
-    int64_t i0 = (int64_t)fi[r], j0 = (int64_t)fj[r];   // int() truncation (values >= 0)
+    // int() truncation of values in [0, src_w) / [0, src_h), both < 2^31
+    // (checked at launch): 32-bit conversions
+    int32_t i0 = (int32_t)fi[r], j0 = (int32_t)fj[r];
     u[r] = fi[r] - (double)i0;
     v[r] = fj[r] - (double)j0;
     ok[r] = true;
     if (INTERP == XRS_INTERP_NEAREST) {
-      if (u[r] > 0.5) i0 = min(max(i0 + 1, (int64_t)0), imax);
-      if (v[r] > 0.5) j0 = min(max(j0 + 1, (int64_t)0), jmax);
+      if (u[r] > 0.5) i0 = (int32_t)min(max((int64_t)i0 + 1, (int64_t)0), imax);
+      if (v[r] > 0.5) j0 = (int32_t)min(max((int64_t)j0 + 1, (int64_t)0), jmax);
     } else {
-      ti1[r] = (int32_t)min(max(i0 + 1, (int64_t)0), imax);
-      tj1[r] = (int32_t)min(max(j0 + 1, (int64_t)0), jmax);
+      ti1[r] = (int32_t)min(max((int64_t)i0 + 1, (int64_t)0), imax);
+      tj1[r] = (int32_t)min(max((int64_t)j0 + 1, (int64_t)0), jmax);
     }
-    ti0[r] = (int32_t)i0;
-    tj0[r] = (int32_t)j0;
+    ti0[r] = i0;
+    tj0[r] = j0;
   }
   for (int64_t s = 0; s < fv.n; ++s) {
     const T* S = src + s * fv.src_sn;
@@ -1165,7 +1169,8 @@ rectify_resolve_kernel(RectArgs a, FusedVar fv) {
             key[r] >>= 1;
           }
           // key / w through the reciprocal, corrected to the exact quotient
-          int64_t j = (int64_t)((double)key[r] * inv_w);
+          // (key < 2^32: a 32-bit conversion, not the long int64 sequence)
+          int64_t j = (int64_t)(uint32_t)((double)key[r] * inv_w);
           int64_t i = (int64_t)key[r] - j * a.w;
           if (i < 0) { --j; i += a.w; } else if (i >= a.w) { ++j; i -= a.w; }
           // a key that is no quad's (inconsistent inputs) is reported and
@@ -1203,7 +1208,9 @@ rectify_resolve_kernel(RectArgs a, FusedVar fv) {
             tri = quad_hit(a, Q[r], dx, dy, det_a, det_b, cu, cv);
           }
           if (tri) {
-            const int64_t li = qi[r] - ti.si0, lj = qj[r] - ti.sj0;   // tile-local quad
+            // tile-local quad (|li|, |lj| < 2^31: int32 -> double converts in
+            // one instruction, int64 -> double takes several)
+            const int32_t li = (int32_t)(qi[r] - ti.si0), lj = (int32_t)(qj[r] - ti.sj0);
             double src_i, src_j;
             if (tri == 1) {
               src_i = (double)li + cu;                                 // src_i0 + clamp(u)
@@ -1496,7 +1503,8 @@ extern "C" int xrs_rectify_var(const double* ij, int64_t ij_sn, int64_t dst_h, i
     return XRS_ERR_NOTIMPL;
   }
   if (!ij || !src || !dst || !err_flags || dst_h < 1 || dst_w < 1 || n < 1 || src_h < 1 || src_w < 1 ||
-      src_sy < src_w || dst_sn < dst_h * dst_w || ij_sn < dst_h * dst_w) {
+      src_sy < src_w || dst_sn < dst_h * dst_w || ij_sn < dst_h * dst_w || src_h > INT32_MAX ||
+      src_w > INT32_MAX) {
     xrs_set_error("xrs_rectify_var: invalid argument");
     return XRS_ERR_ARG;
   }
