@@ -1,7 +1,8 @@
-"""K1 work-shape arms through the test-only knobs (band height, XCD band
-group), timed interleaved on one box against the product shape; every arm's
-raster is compared with the product's bit for bit.
-    python scripts/k1_knob_ab.py [--passes 2] [--steps 20]"""
+"""K1 work-shape arms through the test-only knobs (band height, grid cap in
+blocks per CU = a persistent grid walking the band-major list in lockstep,
+column groups), timed interleaved on one box against the product shape;
+every arm's raster is compared with the product's bit for bit.
+    python scripts/k1_knob_ab.py [--passes 2] [--steps 20] [--arms NAME,...]"""
 from __future__ import annotations
 
 import argparse
@@ -14,15 +15,18 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-ARMS = [("base", 0, 0), ("band8", 8, 0), ("band8_g4", 8, 4), ("band8_g2", 8, 2),
-        ("band16_g2", 16, 0), ("g2", 0, 2), ("band64", 64, 0)]
+# (name, band rows, blocks per CU (0 = one-shot items), column group (0 = bands))
+ARMS = [("base", 0, 0, 0), ("b8p4", 8, 4, 0), ("b8p2", 8, 2, 0), ("b16p4", 16, 4, 0),
+        ("b32p4", 32, 4, 0), ("b4p4", 4, 4, 0), ("b8", 8, 0, 0), ("b16", 16, 0, 0)]
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--passes", type=int, default=2)
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--arms", default="")
     args = ap.parse_args()
+    arms = [a for a in ARMS if not args.arms or a[0] in args.arms.split(",")]
     import bench
     import torch
 
@@ -38,8 +42,9 @@ def main():
     lib = bench.load_benchlib()
     stream = torch.cuda.current_stream(dev)
     for p in range(args.passes):
-        for name, band, group in ARMS:
-            with testing_knob("reproject_band", band), testing_knob("reproject_xcd_group", group):
+        for name, band, bpc, group in arms:
+            with testing_knob("reproject_band", band), testing_knob("reproject_xcd_group", group), \
+                    testing_knob("reproject_blocks_per_cu", bpc):
                 step = lambda: kernels.reproject(src, plan, "bilinear", float("nan"),  # noqa
                                                  out_dtype=np.float32, out=out, flags=flags,
                                                  check=False)
@@ -59,7 +64,8 @@ def main():
             else:
                 same = bool(torch.equal(out.view(torch.int32), ref.view(torch.int32)))
             flags.raise_if_set("k1 arm")
-            print(json.dumps({"arm": name, "band": band or 32, "xcd_group": group or 1,
+            print(json.dumps({"arm": name, "band": band or 32, "blocks_per_cu": bpc,
+                              "column_group": group,
                               "pass": p + 1, "ms_per_launch": round(ms, 4),
                               "bit_equal_to_base": same}), flush=True)
 

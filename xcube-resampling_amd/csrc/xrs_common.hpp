@@ -173,8 +173,11 @@ __device__ inline A window_sum(bool whole, int ny, int nx, F&& val2d) {
 __device__ inline void store_any(void* dst, int64_t idx, int dtype, double fv, int64_t iv,
                                  bool is_int) {
   switch (dtype) {
-    case XRS_DTYPE_F32: static_cast<float*>(dst)[idx] = (float)fv; break;
-    case XRS_DTYPE_F64: static_cast<double*>(dst)[idx] = fv; break;
+    // float results are written once and not read back by the kernel:
+    // non-temporal stores (config 3's K3i 0.208 -> 0.203 ms,
+    // profiles/r04_k3_ab.log)
+    case XRS_DTYPE_F32: __builtin_nontemporal_store((float)fv, static_cast<float*>(dst) + idx); break;
+    case XRS_DTYPE_F64: __builtin_nontemporal_store(fv, static_cast<double*>(dst) + idx); break;
     case XRS_DTYPE_I64: static_cast<int64_t*>(dst)[idx] = is_int ? iv : (int64_t)fv; break;
     case XRS_DTYPE_U8: static_cast<uint8_t*>(dst)[idx] = (uint8_t)iv; break;
     case XRS_DTYPE_I8: static_cast<int8_t*>(dst)[idx] = (int8_t)iv; break;

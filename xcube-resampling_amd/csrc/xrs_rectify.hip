@@ -117,36 +117,6 @@ __device__ inline void monotone_hits(const double* b, int32_t n, double v, int d
   t1 = t - 1;
 }
 
-// The same run [t0, t1] from the estimate's neighbourhood only: the six
-// bounds of tiles e - 1, e, e + 1 are read together (one LDS round trip
-// instead of the walk's dependent reads) and decide t0 / t1 whenever the run's
-// ends fall inside that window — always for evenly spaced tiles with borders
-// narrower than a tile.  Returns false (the caller walks) otherwise.
-__device__ inline bool monotone_hits3(const double* b, int32_t n, double v, int dir,
-                                      const Axis1& est, int32_t& t0, int32_t& t1) {
-  if (v != v) { t0 = 1; t1 = 0; return true; }
-  const double ef = fmin(fmax((v - est.lo0) * est.scale, 0.0), (double)(n - 1));
-  const int32_t e = ef == ef ? (int32_t)ef : 0;
-  const int32_t em = max(e - 1, 0), ep = min(e + 1, n - 1);
-  const double lm = b[2 * em], hm = b[2 * em + 1], le = b[2 * e], he = b[2 * e + 1];
-  const double lp = b[2 * ep], hp = b[2 * ep + 1];
-  // P false..true in t (first true = t0), Q true..false (last true = t1)
-  const bool pm = dir > 0 ? hm >= v : lm <= v, pe = dir > 0 ? he >= v : le <= v;
-  const bool pp = dir > 0 ? hp >= v : lp <= v;
-  const bool qm = dir > 0 ? lm <= v : hm >= v, qe = dir > 0 ? le <= v : he >= v;
-  const bool qp = dir > 0 ? lp <= v : hp >= v;
-  bool ok = true;
-  if (pm) { t0 = em; ok = em == 0; }
-  else if (pe) t0 = e;
-  else if (pp) t0 = ep;
-  else { t0 = n; ok = ep == n - 1; }
-  if (qp) { t1 = ep; ok = ok && ep == n - 1; }
-  else if (qe) t1 = e;
-  else if (qm) t1 = em;
-  else { t1 = -1; ok = ok && em == 0; }
-  return ok;
-}
-
 // +1 / -1 if both interval ends are monotone non-decreasing / non-increasing
 // in t, else 0 (then the candidates are found by a full scan)
 __device__ inline int interval_dir(const double* b, int32_t n) {
@@ -246,15 +216,13 @@ ij_bboxes_kernel(BBoxArgs a, int64_t chunk) {
     int32_t tx0 = 1, tx1 = 0, ty0 = 1, ty1 = 0;
     if (valid && a.ntx > 0) {  // x_min <= x <= x_max, y_min <= y <= y_max (bboxes.py:60-69)
       if (xdir != 0) {
-        if (!monotone_hits3(bx, (int32_t)a.ntx, x, xdir, xest, tx0, tx1))
-          monotone_hits(bx, (int32_t)a.ntx, x, xdir, xest, tx0, tx1);
+        monotone_hits(bx, (int32_t)a.ntx, x, xdir, xest, tx0, tx1);
       } else {
         for (int32_t t = 0; t < (int32_t)a.ntx; ++t)
           if (bx[2 * t] <= x && x <= bx[2 * t + 1]) { if (tx0 > tx1) tx0 = t; tx1 = t; }
       }
       if (ydir != 0) {
-        if (!monotone_hits3(by, (int32_t)a.nty, y, ydir, yest, ty0, ty1))
-          monotone_hits(by, (int32_t)a.nty, y, ydir, yest, ty0, ty1);
+        monotone_hits(by, (int32_t)a.nty, y, ydir, yest, ty0, ty1);
       } else {
         for (int32_t t = 0; t < (int32_t)a.nty; ++t)
           if (by[2 * t] <= y && y <= by[2 * t + 1]) { if (ty0 > ty1) ty0 = t; ty1 = t; }
