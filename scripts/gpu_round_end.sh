@@ -17,7 +17,4 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/p
 cut -c1-200 $OUT/bench_prof.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/rect -o c4 -- python3 scripts/time_rectify.py --reps 10 --fused > $OUT/rect_time.log 2>&1 || exit $?
 grep "ms per" $OUT/rect_time.log
-timeout -k 10 600 python -u scripts/bench_configs.py --configs 1,2,2u,3,4 --cpu-seconds 6 > $OUT/configs.jsonl 2> $OUT/configs.err || exit $?
-cut -c1-140 $OUT/configs.jsonl
-timeout -k 10 300 python -u scripts/rehearse_bands.py > $OUT/bands.jsonl 2> $OUT/bands.err || exit $?
-cut -c1-200 $OUT/bands.jsonl
+# the config lines and the band rehearsal: scripts/gpu_round_end2.sh
