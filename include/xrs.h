@@ -331,6 +331,9 @@ int xrs_rectify_var(const double* ij, int64_t ij_sn, int64_t dst_h, int64_t dst_
  *                                         k-fold (more pixels take the exact test)
  *   XRS_TESTING_REPROJECT_XCD_GROUP       k > 0: K1b deals column groups of k
  *                                         segments instead of whole bands (0)
+ *   XRS_TESTING_RECTIFY_PLAIN_KEYS        1: K5 claims with plain raster keys and
+ *                                         the resolve tests both triangles (the
+ *                                         path of swaths of 2^31 points or more)
  * Returns the previous value (or XRS_ERR_ARG for an unknown knob).
  * ------------------------------------------------------------------------- */
 #define XRS_TESTING_REPROJECT_BAND 1
@@ -339,6 +342,7 @@ int xrs_rectify_var(const double* ij, int64_t ij_sn, int64_t dst_h, int64_t dst_
 #define XRS_TESTING_RECTIFY_EXACT 4
 #define XRS_TESTING_RECTIFY_MARGIN 5
 #define XRS_TESTING_REPROJECT_XCD_GROUP 6
+#define XRS_TESTING_RECTIFY_PLAIN_KEYS 7
 #define XRS_TESTING_NUM_KNOBS 8
 int64_t xrs_testing_set(int knob, int64_t value);
 

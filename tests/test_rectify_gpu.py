@@ -337,6 +337,62 @@ def test_fused_resolve_sampling_equals_k5_then_k6(dtype, interp, n, keep_ij):
     assert np.isfinite(ij.cpu().numpy()).sum() > 0.4 * ij[0].numel() * 2
 
 
+@pytest.mark.parametrize("interp", ["nearest", "bilinear", "triangular"])
+def test_triangle_keys_equal_plain_keys(interp):
+    """The claim records the reference's triangle in the key's low bit and the
+    resolve evaluates that triangle only; swaths of 2^31 points or more keep
+    plain raster keys and test both triangles (forced here by the test knob).
+    Both paths give the same ij image and samples bit for bit, fused and
+    unfused, on a jittered swath with degenerate and NaN-cornered quads, and
+    on a lattice whose points sit on pixel centres (exact edge cases)."""
+    import torch
+
+    import xcube_resampling_amd as xrs
+    from xcube_resampling_amd import kernels
+    from xcube_resampling_amd import rectify as R
+    from xcube_resampling_amd._native import testing_knob
+
+    rng = np.random.default_rng(23)
+    for lattice in (False, True):
+        h, w = 96, 88
+        jj, ii = np.mgrid[0:h, 0:w].astype(np.float64)
+        if lattice:
+            lon = 3.0 + 0.01 * ii + 0.005
+            lat = 40.0 - 0.01 * jj - 0.005
+        else:
+            lon = 3.0 + 0.01 * ii + 0.002 * jj + rng.normal(0, 0.002, (h, w))
+            lat = 40.0 - 0.008 * jj + 0.001 * ii + rng.normal(0, 0.002, (h, w))
+            lon[10, 10:14] = lon[10, 10]
+            lat[50:52, 30] = np.nan
+        sgm = xrs.GridMapping.from_coords(xrs.DataArray(lon, ("y", "x"), name="lon"),
+                                          xrs.DataArray(lat, ("y", "x"), name="lat"),
+                                          "EPSG:4326")
+        res = 0.01 if lattice else 0.006
+        x0 = float(np.floor(np.nanmin(lon) / res) * res)
+        y0 = float(np.floor(np.nanmin(lat) / res) * res)
+        size = (int(np.ceil((np.nanmax(lon) - x0) / res)),
+                int(np.ceil((np.nanmax(lat) - y0) / res)))
+        tgm = xrs.GridMapping.regular(size, (x0, y0), res, "EPSG:4326", tile_size=(40, 36))
+        xy = (torch.from_numpy(lon).cuda(), torch.from_numpy(lat).cuda())
+        src = torch.from_numpy(rng.random((2, h, w)).astype(np.float32)).cuda()
+        tiles = R._device_tiles(sgm, tgm, xy)
+
+        def run():
+            ij = kernels.rectify_ij(xy[0], xy[1], tiles, 0, tgm.height, tgm.width, tgm.x_res,
+                                    -tgm.y_res, 1e-3)
+            ij2, out = kernels.rectify_ij_var(xy[0], xy[1], tiles, tgm.height, tgm.width,
+                                              tgm.x_res, -tgm.y_res, 1e-3, src, interp,
+                                              float("nan"), keep_ij=True)
+            return ij.cpu().numpy(), ij2.cpu().numpy(), out.cpu().numpy()
+
+        got = run()
+        with testing_knob("rectify_plain_keys", 1):
+            exp = run()
+        for g, e, what in zip(got, exp, ("ij", "fused ij", "fused samples")):
+            assert_bitwise_equal(g, e, f"{what} lattice={lattice}")
+        assert np.isfinite(got[0]).sum() > 0.3 * got[0].size
+
+
 def test_rectify_dataset_fused_first_variable():
     """rectify_dataset samples its first device variable inside K5's resolve
     pass whatever its interpolation (rectify.py fuses nearest, bilinear and

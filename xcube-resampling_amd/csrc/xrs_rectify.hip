@@ -1135,8 +1135,12 @@ __device__ inline void sample_rows(const double* fi, const double* fj, int nr,
   }
 }
 
+// Five waves per SIMD (96 VGPRs; 3 values spill to scratch outside the pixel
+// loop): 1.131-1.135 vs 1.156-1.162 ms per config-4 pass at four
+// (profiles/r04_rectify_lb5_ab.log).  Round 3 found 5 slower when the kernel
+// needed 125 VGPRs; 32-bit quad indices and conversions brought it to 98.
 template <typename T, bool FUSE, int INTERP, bool TRI>   // TRI: a.tri_bit (compile time)
-__global__ void __launch_bounds__(kThreads)
+__global__ void __launch_bounds__(kThreads, 5)
 rectify_resolve_kernel(RectArgs a, FusedVar fv) {
   const int64_t n = a.dst_h * a.dst_w;
   const T tfill = FUSE ? Conv<T>::from_f64(fv.fill) : T{};
@@ -1161,7 +1165,7 @@ rectify_resolve_kernel(RectArgs a, FusedVar fv) {
     auto column = [&](int32_t di, uint32_t (&key)[kResolveRows]) {
       const int64_t p0 = (int64_t)(ti.r0 + rb) * a.dst_w + ti.c0 + di;
       Quad Q[kResolveRows];
-      int64_t qj[kResolveRows], qi[kResolveRows];
+      int32_t qj[kResolveRows], qi[kResolveRows];   // < 2^31: h * w < 2^32 checked
       bool tri_b[kResolveRows];   // tri_bit: the claim found the reference's triangle B
 #pragma unroll
       for (int r = 0; r < kResolveRows; ++r) {
@@ -1182,8 +1186,8 @@ rectify_resolve_kernel(RectArgs a, FusedVar fv) {
           const bool ok = j >= 0 && j <= a.h - 2 && i >= 0 && i <= a.w - 2;
           bad |= !ok;
           key[r] = ok ? key[r] : 0xFFFFFFFFu;
-          qj[r] = ok ? j : 0;
-          qi[r] = ok ? i : 0;
+          qj[r] = ok ? (int32_t)j : 0;
+          qi[r] = ok ? (int32_t)i : 0;
           Q[r] = load_quad(a, qj[r], qi[r]);
         }
       }
@@ -1213,7 +1217,7 @@ rectify_resolve_kernel(RectArgs a, FusedVar fv) {
           if (tri) {
             // tile-local quad (|li|, |lj| < 2^31: int32 -> double converts in
             // one instruction, int64 -> double takes several)
-            const int32_t li = (int32_t)(qi[r] - ti.si0), lj = (int32_t)(qj[r] - ti.sj0);
+            const int32_t li = qi[r] - ti.si0, lj = qj[r] - ti.sj0;
             double src_i, src_j;
             if (tri == 1) {
               src_i = (double)li + cu;                                 // src_i0 + clamp(u)
@@ -1403,7 +1407,10 @@ int rectify_ij_impl(const char* what, const double* x, const double* y, int64_t 
   const int64_t widen = xrs_testing_value(XRS_TESTING_RECTIFY_MARGIN);
   a.margin_scale = widen > 1 ? (float)widen : 1.0f;
   a.narrow = (dst_h * dst_w < ((int64_t)1 << 30) && dst_w < ((int64_t)1 << 24)) ? 1 : 0;
-  a.tri_bit = h * w < ((int64_t)1 << 31) ? 1 : 0;
+  // tests: xrs_testing_set(XRS_TESTING_RECTIFY_PLAIN_KEYS, 1) takes the
+  // plain-key path of very large swaths on any input
+  a.tri_bit = h * w < ((int64_t)1 << 31) &&
+              xrs_testing_value(XRS_TESTING_RECTIFY_PLAIN_KEYS) == 0 ? 1 : 0;
   XRS_HIP_CHECK(hipMemsetAsync(keys, 0xFF, (size_t)(dst_h * dst_w) * sizeof(uint32_t), st));
   {
     // as many blocks as are resident at once (fewer when the caller knows a
