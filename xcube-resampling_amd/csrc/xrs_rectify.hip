@@ -313,6 +313,145 @@ ij_bboxes_kernel(BBoxArgs a, int64_t chunk) {
   }
 }
 
+// K4 in grid mode, block-wise.  A wave takes a block of kBoxBlockRows source
+// rows x 64 columns (lane l: column l, one pixel per row).  The wave's bbox of
+// the coordinates (NaN skipped) selects the candidate tiles; for each one:
+//  * every pixel of the block valid (no NaN coordinate) and the block's bbox
+//    inside the tile's box: every pixel passes the reference's test
+//    (x_min <= x <= x_max, y_min <= y <= y_max, bboxes.py:60-69), so the
+//    block's whole index range is the tile's contribution;
+//  * otherwise the reference's test per pixel, and the extremes from ballots:
+//    the first / last lane with a pixel inside give i, the first / last row
+//    with one give j (no cross-lane reductions).
+// The extremes equal the per-pixel scan's.  Most blocks lie inside one tile;
+// the per-pixel path is taken near tile edges (the boxes overlap by the
+// border), so a pixel costs a few instructions instead of a tile search and a
+// wave merge.  Boxes whose intervals are not monotone (never for a tile grid)
+// make every tile a candidate: slow, same result.
+constexpr int kBoxBlockRows = 4;
+
+__device__ inline double wave_fmin_f64(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ inline double wave_fmax_f64(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+template <bool SHARED>
+__global__ void __launch_bounds__(kThreads)
+ij_bboxes_block_kernel(BBoxArgs a) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int64_t nbx = 2 * a.ntx, nby = 2 * a.nty;
+  double* sbx = reinterpret_cast<double*>(smem);
+  double* sby = sbx + nbx;
+  int32_t* sacc = reinterpret_cast<int32_t*>(sby + nby);
+  const double* bx = a.bx;
+  const double* by = a.by;
+  int32_t* acc = a.acc;
+  if (SHARED) {
+    for (int64_t i = threadIdx.x; i < nbx; i += kThreads) sbx[i] = a.bx[i];
+    for (int64_t i = threadIdx.x; i < nby; i += kThreads) sby[i] = a.by[i];
+    for (int64_t i = threadIdx.x; i < 4 * a.nboxes; i += kThreads)
+      sacc[i] = (i & 3) < 2 ? INT32_MAX : -1;
+    __syncthreads();
+    bx = sbx;
+    by = sby;
+    acc = sacc;
+  }
+  const int32_t ntx = (int32_t)a.ntx, nty = (int32_t)a.nty;
+  const int xdir = interval_dir(bx, ntx), ydir = interval_dir(by, nty);
+  const Axis1 xest = axis_estimate(bx, ntx), yest = axis_estimate(by, nty);
+  const int lane = threadIdx.x & 63;
+  const int64_t ncb = (a.w + 63) / 64, nrb = (a.h + kBoxBlockRows - 1) / kBoxBlockRows;
+  const int64_t nblk = ncb * nrb;
+  const int64_t nwaves = (int64_t)gridDim.x * (kThreads / 64);
+  for (int64_t blk = (int64_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6); blk < nblk;
+       blk += nwaves) {   // wave-uniform
+    const int64_t rb = blk / ncb, cb = blk - rb * ncb;
+    const int32_t i0 = (int32_t)(cb * 64), j0 = (int32_t)(rb * kBoxBlockRows);
+    const int32_t i = i0 + lane;
+    const bool col_ok = i < a.w;
+    const int nrows = (int)min((int64_t)kBoxBlockRows, a.h - j0);
+    double x[kBoxBlockRows], y[kBoxBlockRows];
+#pragma unroll
+    for (int r = 0; r < kBoxBlockRows; ++r) {
+      x[r] = y[r] = NAN;
+      if (col_ok && r < nrows) {
+        const int64_t o = (int64_t)(j0 + r) * a.sy + i;
+        x[r] = a.x[o];
+        y[r] = a.y[o];
+      }
+    }
+    double xmn = x[0], xmx = x[0], ymn = y[0], ymx = y[0];
+    bool nan = col_ok && (x[0] != x[0] || y[0] != y[0]);
+#pragma unroll
+    for (int r = 1; r < kBoxBlockRows; ++r) {
+      xmn = fmin(xmn, x[r]); xmx = fmax(xmx, x[r]);
+      ymn = fmin(ymn, y[r]); ymx = fmax(ymx, y[r]);
+      nan = nan || (col_ok && r < nrows && (x[r] != x[r] || y[r] != y[r]));
+    }
+    xmn = wave_fmin_f64(xmn); xmx = wave_fmax_f64(xmx);
+    ymn = wave_fmin_f64(ymn); ymx = wave_fmax_f64(ymx);
+    if (xmn != xmn || ymn != ymn) continue;   // no finite pixel (wave-uniform)
+    const bool all_valid = __ballot(nan) == 0;
+    // candidate tiles: intervals intersecting [xmn, xmx] x [ymn, ymx]
+    int32_t tx0 = 0, tx1 = ntx - 1, ty0 = 0, ty1 = nty - 1, d0, d1;
+    if (xdir > 0) { monotone_hits(bx, ntx, xmn, xdir, xest, tx0, d1); monotone_hits(bx, ntx, xmx, xdir, xest, d0, tx1); }
+    if (xdir < 0) { monotone_hits(bx, ntx, xmx, xdir, xest, tx0, d1); monotone_hits(bx, ntx, xmn, xdir, xest, d0, tx1); }
+    if (ydir > 0) { monotone_hits(by, nty, ymn, ydir, yest, ty0, d1); monotone_hits(by, nty, ymx, ydir, yest, d0, ty1); }
+    if (ydir < 0) { monotone_hits(by, nty, ymx, ydir, yest, ty0, d1); monotone_hits(by, nty, ymn, ydir, yest, d0, ty1); }
+    tx0 = __builtin_amdgcn_readfirstlane(tx0); tx1 = __builtin_amdgcn_readfirstlane(tx1);
+    ty0 = __builtin_amdgcn_readfirstlane(ty0); ty1 = __builtin_amdgcn_readfirstlane(ty1);
+    const int32_t ilast = (int32_t)min((int64_t)i0 + 63, a.w - 1);
+    for (int32_t ty = ty0; ty <= ty1; ++ty) {
+      const double ylo = by[2 * ty], yhi = by[2 * ty + 1];
+      for (int32_t tx = tx0; tx <= tx1; ++tx) {
+        const double xlo = bx[2 * tx], xhi = bx[2 * tx + 1];
+        const int32_t k = ty * ntx + tx;
+        int32_t imin, jmin, imax, jmax;
+        if (all_valid && xlo <= xmn && xmx <= xhi && ylo <= ymn && ymx <= yhi) {
+          imin = i0; imax = ilast; jmin = j0; jmax = j0 + nrows - 1;
+        } else {
+          bool any = false;
+          int32_t rmask = 0;
+#pragma unroll
+          for (int r = 0; r < kBoxBlockRows; ++r) {
+            const bool in = xlo <= x[r] && x[r] <= xhi && ylo <= y[r] && y[r] <= yhi;
+            any = any || in;
+            rmask |= __ballot(in) != 0 ? (1 << r) : 0;
+          }
+          const uint64_t lanes = __ballot(any);
+          if (lanes == 0) continue;   // wave-uniform
+          imin = i0 + __builtin_ctzll(lanes);
+          imax = i0 + 63 - __builtin_clzll(lanes);
+          jmin = j0 + __builtin_ctz(rmask);
+          jmax = j0 + 31 - __builtin_clz(rmask);
+        }
+        if (lane == 0) {
+          atomicMin(&acc[4 * k + 0], imin);
+          atomicMin(&acc[4 * k + 1], jmin);
+          atomicMax(&acc[4 * k + 2], imax);
+          atomicMax(&acc[4 * k + 3], jmax);
+        }
+      }
+    }
+  }
+  if (SHARED) {
+    __syncthreads();
+    for (int64_t k = threadIdx.x; k < a.nboxes; k += kThreads) {
+      if (sacc[4 * k + 2] < 0) continue;  // box not touched by this block
+      atomicMin(&a.acc[4 * k + 0], sacc[4 * k + 0]);
+      atomicMin(&a.acc[4 * k + 1], sacc[4 * k + 1]);
+      atomicMax(&a.acc[4 * k + 2], sacc[4 * k + 2]);
+      atomicMax(&a.acc[4 * k + 3], sacc[4 * k + 3]);
+    }
+  }
+}
+
 // ---- rectify geometry (rectify.py:737-773) -----------------------------------
 __device__ inline double fdet(double px0, double py0, double px1, double py1, double px2,
                               double py2) {
@@ -1369,6 +1508,17 @@ extern "C" int xrs_ij_bboxes(const double* x, const double* y, int64_t h, int64_
   const int nb = grid_blocks(h * w, kThreads, 256 * 8);
   const int64_t chunk = ((h * w + nb - 1) / nb + kThreads - 1) / kThreads * kThreads;
   const int64_t lds = (ntx > 0 ? 16 * (ntx + nty) : 32 * nboxes) + 16 * nboxes;
+  if (ntx > 0) {   // a tile grid: block-wise (ij_bboxes_block_kernel)
+    const int64_t nwave = ((w + 63) / 64) * ((h + kBoxBlockRows - 1) / kBoxBlockRows);
+    const int nbb = grid_blocks(nwave, kThreads / 64, 256 * 8);
+    if (lds <= 48 * 1024)
+      hipLaunchKernelGGL(ij_bboxes_block_kernel<true>, dim3(nbb), dim3(kThreads), (size_t)lds, st,
+                         a);
+    else
+      hipLaunchKernelGGL(ij_bboxes_block_kernel<false>, dim3(nbb), dim3(kThreads), 0, st, a);
+    XRS_HIP_CHECK(hipGetLastError());
+    return XRS_OK;
+  }
   if (lds <= 48 * 1024)
     hipLaunchKernelGGL(ij_bboxes_kernel<true>, dim3(nb), dim3(kThreads), (size_t)lds, st, a,
                        chunk);
