@@ -327,8 +327,10 @@ ij_bboxes_kernel(BBoxArgs a, int64_t chunk) {
 // the per-pixel path is taken near tile edges (the boxes overlap by the
 // border), so a pixel costs a few instructions instead of a tile search and a
 // wave merge.  Boxes whose intervals are not monotone (never for a tile grid)
-// make every tile a candidate: slow, same result.
-constexpr int kBoxBlockRows = 4;
+// make every tile a candidate: slow, same result.  16 rows measured best at
+// config 4 (K4 124 -> 92 us against 4 rows; 2 / 8 rows slower or equal,
+// profiles/r04_rectify_k4_rows_ab.log).
+constexpr int kBoxBlockRows = 16;
 
 __device__ inline double wave_fmin_f64(double v) {
 #pragma unroll
