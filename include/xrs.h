@@ -239,6 +239,16 @@ int xrs_ij_bboxes(const double* x, const double* y, int64_t h, int64_t w, int64_
                   int64_t nboxes, int64_t ntx, int64_t nty, const double* bx,
                   const double* by, int32_t* acc, void* stream);
 
+/* xrs_ij_bboxes_fill — xrs_ij_bboxes whose grid also sets fill_words 32-bit
+ * words at `fill` (16-byte aligned) to 0xFFFFFFFF: the claim-key scratch of
+ * the xrs_rectify_ij / _ij_var call that follows on the same stream
+ * (keys_ready = 1), filled while K4 streams the coordinates instead of in a
+ * pass of its own.  fill_words = 0: exactly xrs_ij_bboxes. */
+int xrs_ij_bboxes_fill(const double* x, const double* y, int64_t h, int64_t w, int64_t sy,
+                       int64_t nboxes, int64_t ntx, int64_t nty, const double* bx,
+                       const double* by, int32_t* acc, uint32_t* fill, int64_t fill_words,
+                       void* stream);
+
 /* -------------------------------------------------------------------------
  * xrs_rectify_ij — replaces _compute_target_source_ij_block and the numba
  * kernels _compute_target_source_ij_sequential/_line (rectify.py:373-576):
@@ -260,13 +270,16 @@ int xrs_ij_bboxes(const double* x, const double* y, int64_t h, int64_t w, int64_
  * x_scale = dst_x_res; y_scale = dst_y_res (j-axis up) or -dst_y_res.
  * keys: (dst_h, dst_w) uint32 scratch; ij: (2, dst_h, dst_w) float64 output
  *   (NaN where no quad hits).
+ * keys_ready: 0 — the call sets keys to 0xFFFFFFFF first (on `stream`);
+ *   1 — keys already hold 0xFFFFFFFF everywhere, ordered before this call
+ *   (xrs_ij_bboxes_fill).  A claim pass consumes the fill.
  * ------------------------------------------------------------------------- */
 int xrs_rectify_ij(const double* x, const double* y, int64_t h, int64_t w, int64_t sy,
                    const void* tiles, int64_t ntiles, int64_t ntiles_x,
                    const int64_t* chunk_offsets, int64_t max_chunks,
                    int64_t dst_h, int64_t dst_w, double x_scale, double y_scale,
-                   double uv_delta, uint32_t* keys, double* ij, int32_t* err_flags,
-                   void* stream);
+                   double uv_delta, uint32_t* keys, int keys_ready, double* ij,
+                   int32_t* err_flags, void* stream);
 
 /* -------------------------------------------------------------------------
  * xrs_rectify_ij_var — xrs_rectify_ij with the first variable sampled by the
@@ -280,8 +293,8 @@ int xrs_rectify_ij(const double* x, const double* y, int64_t h, int64_t w, int64
 int xrs_rectify_ij_var(const double* x, const double* y, int64_t h, int64_t w, int64_t sy,
                        const void* tiles, int64_t ntiles, const int64_t* chunk_offsets,
                        int64_t max_chunks, int64_t dst_h, int64_t dst_w, double x_scale,
-                       double y_scale, double uv_delta, uint32_t* keys, double* ij,
-                       const void* src, int src_dtype, int64_t n, int64_t src_h, int64_t src_w,
+                       double y_scale, double uv_delta, uint32_t* keys, int keys_ready,
+                       double* ij, const void* src, int src_dtype, int64_t n, int64_t src_h, int64_t src_w,
                        int64_t src_sn, int64_t src_sy, void* dst, int64_t dst_sn, int interp,
                        double fill, int32_t* err_flags, void* stream);
 

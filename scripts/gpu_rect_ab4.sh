@@ -7,8 +7,9 @@ timeout -k 10 600 python -u -m pytest tests/test_rectify_gpu.py tests/test_gridm
 tail -1 $O/pytest.log
 for pass in 1 2 3; do
   for arm in product "$@"; do
-    if [ $arm = product ]; then L=""; else L=$PWD/probe/$arm/pkg/lib/libxrs.so; fi
-    XRS_LIBRARY=$L timeout -k 10 120 python -u scripts/time_rectify.py --reps 20 --fused > $O/t_${arm}_$pass.log 2>&1 || exit $?
+    P=""
+    if [ $arm = product ]; then L=""; elif [ -d probe/$arm/root ]; then L=""; P=$PWD/probe/$arm/root; else L=$PWD/probe/$arm/pkg/lib/libxrs.so; fi
+    XRS_PYROOT=$P XRS_LIBRARY=$L timeout -k 10 120 python -u scripts/time_rectify.py --reps 20 --fused > $O/t_${arm}_$pass.log 2>&1 || exit $?
     echo "$arm $pass $(grep 'ms per' $O/t_${arm}_$pass.log)"
   done
 done

@@ -12,7 +12,9 @@ import sys
 
 import numpy as np
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+# XRS_PYROOT: the package from another tree (an A/B arm of the host code)
+sys.path.insert(0, os.environ.get("XRS_PYROOT") or
+                os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def main():

@@ -69,10 +69,11 @@ def test_product_library_reads_no_environment():
 
 
 def test_argument_errors_are_reported_before_any_device_work():
-    """xrs_reproject / xrs_reproject_proj validate their arguments on the host
-    and return XRS_ERR_ARG with a message (no HIP call is made): a float64
-    source row above 2 GiB (K1 addresses rows as buffer resources) and an
-    unsupported projection pipeline."""
+    """xrs_reproject / xrs_reproject_proj / xrs_ij_bboxes_fill validate their
+    arguments on the host and return XRS_ERR_ARG with a message (no HIP call
+    is made): a float64 source row above 2 GiB (K1 addresses rows as buffer
+    resources), an unsupported projection pipeline, a fill scratch that is
+    missing or not 16-byte aligned."""
     import ctypes
 
     from xcube_resampling_amd import _native
@@ -92,6 +93,13 @@ def test_argument_errors_are_reported_before_any_device_work():
                                 fake, fake, fake, 4, 4, 1.0, 1.0, 0, 0.0, fake, None)
     assert rc == _native.XRS_ERR_ARG
     assert b"pipeline" in lib.xrs_last_error()
+    # K4's claim-key fill needs a 16-byte aligned scratch (non-temporal
+    # 16-byte stores)
+    rc = lib.xrs_ij_bboxes_fill(fake, fake, 4, 4, 4, 1, 0, 0, fake, fake, fake,
+                                ctypes.c_void_p(4096 + 4), 16, None)
+    assert rc == _native.XRS_ERR_ARG
+    rc = lib.xrs_ij_bboxes_fill(fake, fake, 4, 4, 4, 1, 0, 0, fake, fake, fake, None, 16, None)
+    assert rc == _native.XRS_ERR_ARG
 
 
 def test_library_override_limited_to_probe_arms(tmp_path):

@@ -393,6 +393,64 @@ def test_triangle_keys_equal_plain_keys(interp):
         assert np.isfinite(got[0]).sum() > 0.3 * got[0].size
 
 
+def test_k4_filled_claim_keys_equal_in_call_fill():
+    """K4 fills the claim-key scratch beside the coordinate scan
+    (xrs_ij_bboxes_fill; DeviceTiles hands it to the first K5 call, which
+    passes keys_ready = 1); later calls with the same tiles fill their own.
+    Same ij and fused samples bit for bit; the fill itself sets every word,
+    16-byte body and word tail, and leaves K4's accumulators unchanged."""
+    import torch
+
+    import xcube_resampling_amd as xrs
+    from xcube_resampling_amd import kernels
+    from xcube_resampling_amd import rectify as R
+
+    rng = np.random.default_rng(31)
+    h, w = 140, 121
+    jj, ii = np.mgrid[0:h, 0:w].astype(np.float64)
+    lon = 3.0 + 0.01 * ii + 0.002 * jj + rng.normal(0, 0.002, (h, w))
+    lat = 40.0 - 0.008 * jj + 0.001 * ii + rng.normal(0, 0.002, (h, w))
+    sgm = xrs.GridMapping.from_coords(xrs.DataArray(lon, ("y", "x"), name="lon"),
+                                      xrs.DataArray(lat, ("y", "x"), name="lat"), "EPSG:4326")
+    res = 0.006
+    x0 = float(np.floor(lon.min() / res) * res)
+    y0 = float(np.floor(lat.min() / res) * res)
+    size = (int(np.ceil((lon.max() - x0) / res)), int(np.ceil((lat.max() - y0) / res)))
+    tgm = xrs.GridMapping.regular(size, (x0, y0), res, "EPSG:4326", tile_size=(48, 40))
+    xy = (torch.from_numpy(lon).cuda(), torch.from_numpy(lat).cuda())
+    src = torch.from_numpy(rng.random((1, h, w)).astype(np.float32)).cuda()
+
+    def ij_of(t):
+        return kernels.rectify_ij(xy[0], xy[1], t, 0, tgm.height, tgm.width, tgm.x_res,
+                                  -tgm.y_res, 1e-3).cpu().numpy()
+
+    def fused_of(t):
+        return kernels.rectify_ij_var(xy[0], xy[1], t, tgm.height, tgm.width, tgm.x_res,
+                                      -tgm.y_res, 1e-3, src, "bilinear", float("nan"),
+                                      keep_ij=False)[1].cpu().numpy()
+
+    for run in (ij_of, fused_of):
+        t = R._device_tiles(sgm, tgm, xy)
+        assert isinstance(t, kernels.DeviceTiles) and t._keys is not None
+        got = run(t)               # K4's fill (keys_ready = 1)
+        assert t._keys is None     # consumed
+        again = run(t)             # the call's own fill
+        assert_bitwise_equal(got, again, run.__name__)
+    assert np.isfinite(ij_of(R._device_tiles(sgm, tgm, xy))).mean() > 0.3
+
+    # the fill: odd word counts (16-byte body + tail), accumulators as without
+    boxes = np.asarray(tgm.xy_bboxes, np.float64)
+    grid = (len(range(0, tgm.width, tgm.tile_width)), len(range(0, tgm.height, tgm.tile_height)))
+    plain, _, _, _ = kernels._ij_bboxes_launch(xy[0], xy[1], boxes, 0.01, grid, None, None)
+    for words in (1, 5, 4099):
+        buf = torch.zeros(words + 8, dtype=torch.int32, device="cuda")
+        acc, _, _, _ = kernels._ij_bboxes_launch(xy[0], xy[1], boxes, 0.01, grid, None, None,
+                                                 fill=buf[4:4 + words])
+        b = buf.cpu().numpy()
+        assert (b[4:4 + words] == -1).all() and (b[:4] == 0).all() and (b[4 + words:] == 0).all()
+        assert_bitwise_equal(acc.cpu().numpy(), plain.cpu().numpy(), f"acc fill={words}")
+
+
 def test_rectify_dataset_fused_first_variable():
     """rectify_dataset samples its first device variable inside K5's resolve
     pass whatever its interpolation (rectify.py fuses nearest, bilinear and

@@ -120,12 +120,14 @@ _SIGNATURES = {
     "xrs_any_nan": (_c_int, [_c_ptr, _c_int, _c_i64, _c_ptr, _c_ptr]),
     "xrs_ij_bboxes": (_c_int, [_c_ptr, _c_ptr, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64,
                                _c_ptr, _c_ptr, _c_ptr, _c_ptr]),
+    "xrs_ij_bboxes_fill": (_c_int, [_c_ptr, _c_ptr, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64,
+                                    _c_i64, _c_ptr, _c_ptr, _c_ptr, _c_ptr, _c_i64, _c_ptr]),
     "xrs_rectify_ij": (_c_int, [_c_ptr, _c_ptr, _c_i64, _c_i64, _c_i64, _c_ptr, _c_i64, _c_i64,
                                 _c_ptr, _c_i64, _c_i64, _c_i64, _c_dbl, _c_dbl, _c_dbl,
-                                _c_ptr, _c_ptr, _c_ptr, _c_ptr]),
+                                _c_ptr, _c_int, _c_ptr, _c_ptr, _c_ptr]),   # keys, keys_ready, ij
     "xrs_rectify_ij_var": (_c_int, [_c_ptr, _c_ptr, _c_i64, _c_i64, _c_i64, _c_ptr, _c_i64,
                                     _c_ptr, _c_i64, _c_i64, _c_i64, _c_dbl, _c_dbl, _c_dbl,
-                                    _c_ptr, _c_ptr,                                    # keys, ij
+                                    _c_ptr, _c_int, _c_ptr,                # keys, keys_ready, ij
                                     _c_ptr, _c_int, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64,
                                     _c_ptr, _c_i64, _c_int, _c_dbl, _c_ptr, _c_ptr]),
     "xrs_rectify_tiles": (_c_int, [_c_ptr, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64,

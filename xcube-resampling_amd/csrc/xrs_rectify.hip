@@ -60,7 +60,41 @@ struct BBoxArgs {
   const double* bx;       // grid: (ntx, 2) [x_min, x_max] (border included); else (nboxes, 4)
   const double* by;       // grid: (nty, 2) [y_min, y_max]
   int32_t* acc;           // (nboxes, 4): min i, min j, max i, max j
+  uint32_t* fill;         // NULL or 16-byte aligned: fill_words words set to ~0
+  int64_t fill_words;     // (the claim-key scratch of the K5 that follows)
 };
+
+// The claim-key scratch filled by K4's own grid: K4 reads the coordinates at
+// well under the HBM rate, so the writes ride along instead of taking a
+// memset pass of their own between K4 and the claim.  Non-temporal 16-byte
+// stores; kFillAt: 0 = all of a thread's share first, 1 = after its
+// blocks, 2 = a block's share of the scratch with each source block (the
+// block kernel; the per-pixel kernel fills first).
+constexpr int kFillAt = 2;
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ inline void fill_scratch(const BBoxArgs& a) {
+  if (!a.fill) return;
+  const u32x4 v = {~0u, ~0u, ~0u, ~0u};
+  const int64_t nt = (int64_t)gridDim.x * blockDim.x;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t n4 = a.fill_words >> 2;
+  u32x4* f4 = reinterpret_cast<u32x4*>(a.fill);
+  for (int64_t k = t; k < n4; k += nt) __builtin_nontemporal_store(v, f4 + k);
+  for (int64_t k = (n4 << 2) + t; k < a.fill_words; k += nt) a.fill[k] = ~0u;
+}
+
+// share [blk * per, (blk + 1) * per) of the scratch's 16-byte words, one
+// wave (lane = 0..63); the word tail (fill_words % 4) goes with block 0
+__device__ inline void fill_scratch_block(const BBoxArgs& a, int64_t blk, int64_t per,
+                                          int lane) {
+  const u32x4 v = {~0u, ~0u, ~0u, ~0u};
+  const int64_t n4 = a.fill_words >> 2;
+  const int64_t e = min((blk + 1) * per, n4);
+  u32x4* f4 = reinterpret_cast<u32x4*>(a.fill);
+  for (int64_t k = blk * per + lane; k < e; k += 64) __builtin_nontemporal_store(v, f4 + k);
+  if (blk == 0 && lane < (a.fill_words & 3)) a.fill[(n4 << 2) + lane] = ~0u;
+}
 
 // Next candidate box > `after` that contains (x, y), or INT32_MAX.
 __device__ inline int32_t next_box(const BBoxArgs& a, const double* bx, double x, double y,
@@ -137,6 +171,7 @@ template <bool SHARED>
 __global__ void __launch_bounds__(kThreads)
 ij_bboxes_kernel(BBoxArgs a, int64_t chunk) {
   extern __shared__ __align__(16) unsigned char smem[];
+  fill_scratch(a);
   const int64_t nbx = a.ntx > 0 ? 2 * a.ntx : 4 * a.nboxes;   // doubles of bx
   const int64_t nby = a.ntx > 0 ? 2 * a.nty : 0;
   double* sbx = reinterpret_cast<double*>(smem);
@@ -347,6 +382,7 @@ template <bool SHARED>
 __global__ void __launch_bounds__(kThreads)
 ij_bboxes_block_kernel(BBoxArgs a) {
   extern __shared__ __align__(16) unsigned char smem[];
+  if (kFillAt == 0) fill_scratch(a);
   const int64_t nbx = 2 * a.ntx, nby = 2 * a.nty;
   double* sbx = reinterpret_cast<double*>(smem);
   double* sby = sbx + nbx;
@@ -371,6 +407,7 @@ ij_bboxes_block_kernel(BBoxArgs a) {
   const int64_t ncb = (a.w + 63) / 64, nrb = (a.h + kBoxBlockRows - 1) / kBoxBlockRows;
   const int64_t nblk = ncb * nrb;
   const int64_t nwaves = (int64_t)gridDim.x * (kThreads / 64);
+  const int64_t fill_per = ((a.fill_words >> 2) + nblk - 1) / nblk;
   for (int64_t blk = (int64_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6); blk < nblk;
        blk += nwaves) {   // wave-uniform
     const int64_t rb = blk / ncb, cb = blk - rb * ncb;
@@ -388,6 +425,7 @@ ij_bboxes_block_kernel(BBoxArgs a) {
         y[r] = a.y[o];
       }
     }
+    if (kFillAt == 2 && a.fill) fill_scratch_block(a, blk, fill_per, lane);
     double xmn = x[0], xmx = x[0], ymn = y[0], ymx = y[0];
     bool nan = col_ok && (x[0] != x[0] || y[0] != y[0]);
 #pragma unroll
@@ -442,6 +480,7 @@ ij_bboxes_block_kernel(BBoxArgs a) {
       }
     }
   }
+  if (kFillAt == 1) fill_scratch(a);
   if (SHARED) {
     __syncthreads();
     for (int64_t k = threadIdx.x; k < a.nboxes; k += kThreads) {
@@ -1495,18 +1534,25 @@ extern "C" int xrs_rectify_tiles(const int32_t* acc, int64_t ntiles_x, int64_t n
   return XRS_OK;
 }
 
-extern "C" int xrs_ij_bboxes(const double* x, const double* y, int64_t h, int64_t w,
-                             int64_t sy, int64_t nboxes, int64_t ntx, int64_t nty,
-                             const double* bx, const double* by, int32_t* acc, void* stream) {
+extern "C" int xrs_ij_bboxes_fill(const double* x, const double* y, int64_t h, int64_t w,
+                                  int64_t sy, int64_t nboxes, int64_t ntx, int64_t nty,
+                                  const double* bx, const double* by, int32_t* acc,
+                                  uint32_t* fill, int64_t fill_words, void* stream) {
   using namespace xrs;
   if (!x || !y || !bx || !acc || h < 1 || w < 1 || sy < w || nboxes < 0 ||
-      (ntx > 0 && (ntx * nty != nboxes || !by)) || h * w > INT32_MAX) {
+      (ntx > 0 && (ntx * nty != nboxes || !by)) || h * w > INT32_MAX || fill_words < 0 ||
+      (fill_words > 0 && (!fill || (reinterpret_cast<uintptr_t>(fill) & 15) != 0))) {
     xrs_set_error("xrs_ij_bboxes: invalid argument");
     return XRS_ERR_ARG;
   }
-  if (nboxes == 0) return XRS_OK;
-  BBoxArgs a{x, y, h, w, sy, nboxes, ntx, nty, bx, by, acc};
   hipStream_t st = static_cast<hipStream_t>(stream);
+  if (nboxes == 0) {
+    if (fill_words > 0)
+      XRS_HIP_CHECK(hipMemsetAsync(fill, 0xFF, (size_t)fill_words * sizeof(uint32_t), st));
+    return XRS_OK;
+  }
+  BBoxArgs a{x, y, h, w, sy, nboxes, ntx, nty, bx, by, acc, fill_words > 0 ? fill : nullptr,
+             fill_words};
   const int nb = grid_blocks(h * w, kThreads, 256 * 8);
   const int64_t chunk = ((h * w + nb - 1) / nb + kThreads - 1) / kThreads * kThreads;
   const int64_t lds = (ntx > 0 ? 16 * (ntx + nty) : 32 * nboxes) + 16 * nboxes;
@@ -1530,13 +1576,20 @@ extern "C" int xrs_ij_bboxes(const double* x, const double* y, int64_t h, int64_
   return XRS_OK;
 }
 
+extern "C" int xrs_ij_bboxes(const double* x, const double* y, int64_t h, int64_t w,
+                             int64_t sy, int64_t nboxes, int64_t ntx, int64_t nty,
+                             const double* bx, const double* by, int32_t* acc, void* stream) {
+  return xrs_ij_bboxes_fill(x, y, h, w, sy, nboxes, ntx, nty, bx, by, acc, nullptr, 0, stream);
+}
+
 namespace xrs {
 namespace {
 int rectify_ij_impl(const char* what, const double* x, const double* y, int64_t h, int64_t w,
                     int64_t sy, const void* tiles, int64_t ntiles, const int64_t* chunk_offsets,
                     int64_t max_chunks, int64_t dst_h, int64_t dst_w, double x_scale,
-                    double y_scale, double uv_delta, uint32_t* keys, double* ij,
-                    int32_t* err_flags, const FusedVar* fv, int fv_dtype, hipStream_t st) {
+                    double y_scale, double uv_delta, uint32_t* keys, int keys_ready,
+                    double* ij, int32_t* err_flags, const FusedVar* fv, int fv_dtype,
+                    hipStream_t st) {
   if (!x || !y || !tiles || !keys || (!ij && !(fv && !fv->write_ij)) || !err_flags || h < 2 ||
       w < 2 || sy < w || ntiles < 1 || dst_h < 1 || dst_w < 1 || h * w >= (int64_t)UINT32_MAX ||
       !chunk_offsets || max_chunks < 0 || dst_h > INT32_MAX || dst_w > INT32_MAX) {
@@ -1563,7 +1616,8 @@ int rectify_ij_impl(const char* what, const double* x, const double* y, int64_t 
   // plain-key path of very large swaths on any input
   a.tri_bit = h * w < ((int64_t)1 << 31) &&
               xrs_testing_value(XRS_TESTING_RECTIFY_PLAIN_KEYS) == 0 ? 1 : 0;
-  XRS_HIP_CHECK(hipMemsetAsync(keys, 0xFF, (size_t)(dst_h * dst_w) * sizeof(uint32_t), st));
+  if (!keys_ready)   // else filled by K4 (xrs_ij_bboxes_fill) or the caller
+    XRS_HIP_CHECK(hipMemsetAsync(keys, 0xFF, (size_t)(dst_h * dst_w) * sizeof(uint32_t), st));
   {
     // as many blocks as are resident at once (fewer when the caller knows a
     // smaller strip count)
@@ -1626,20 +1680,22 @@ extern "C" int xrs_rectify_ij(const double* x, const double* y, int64_t h, int64
                               int64_t sy, const void* tiles, int64_t ntiles, int64_t ntiles_x,
                               const int64_t* chunk_offsets, int64_t max_chunks,
                               int64_t dst_h, int64_t dst_w, double x_scale,
-                              double y_scale, double uv_delta, uint32_t* keys, double* ij,
-                              int32_t* err_flags, void* stream) {
+                              double y_scale, double uv_delta, uint32_t* keys,
+                              int keys_ready, double* ij, int32_t* err_flags, void* stream) {
   (void)ntiles_x;
   return xrs::rectify_ij_impl("xrs_rectify_ij", x, y, h, w, sy, tiles, ntiles, chunk_offsets,
-                              max_chunks, dst_h, dst_w, x_scale, y_scale, uv_delta, keys, ij,
-                              err_flags, nullptr, 0, static_cast<hipStream_t>(stream));
+                              max_chunks, dst_h, dst_w, x_scale, y_scale, uv_delta, keys,
+                              keys_ready, ij, err_flags, nullptr, 0,
+                              static_cast<hipStream_t>(stream));
 }
 
 extern "C" int xrs_rectify_ij_var(const double* x, const double* y, int64_t h, int64_t w,
                                   int64_t sy, const void* tiles, int64_t ntiles,
                                   const int64_t* chunk_offsets, int64_t max_chunks,
                                   int64_t dst_h, int64_t dst_w, double x_scale, double y_scale,
-                                  double uv_delta, uint32_t* keys, double* ij,
-                                  const void* src, int src_dtype, int64_t n, int64_t src_h,
+                                  double uv_delta, uint32_t* keys, int keys_ready,
+                                  double* ij, const void* src, int src_dtype, int64_t n,
+                                  int64_t src_h,
                                   int64_t src_w, int64_t src_sn, int64_t src_sy, void* dst,
                                   int64_t dst_sn, int interp, double fill,
                                   int32_t* err_flags, void* stream) {
@@ -1657,8 +1713,9 @@ extern "C" int xrs_rectify_ij_var(const double* x, const double* y, int64_t h, i
   const FusedVar fv{src, n, src_h, src_w, src_sn, src_sy, dst, dst_sn, fill, interp,
                     ij != nullptr ? 1 : 0};
   return rectify_ij_impl("xrs_rectify_ij_var", x, y, h, w, sy, tiles, ntiles, chunk_offsets,
-                         max_chunks, dst_h, dst_w, x_scale, y_scale, uv_delta, keys, ij,
-                         err_flags, &fv, src_dtype, static_cast<hipStream_t>(stream));
+                         max_chunks, dst_h, dst_w, x_scale, y_scale, uv_delta, keys,
+                         keys_ready, ij, err_flags, &fv, src_dtype,
+                         static_cast<hipStream_t>(stream));
 }
 
 extern "C" int xrs_rectify_var(const double* ij, int64_t ij_sn, int64_t dst_h, int64_t dst_w,

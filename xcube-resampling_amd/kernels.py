@@ -160,9 +160,10 @@ def _upload_small(arr: np.ndarray, device, stream):
     return to_device(np.ascontiguousarray(arr), device)
 
 
-def _ij_bboxes_launch(x_image, y_image, xy_bboxes, xy_border, grid, device, stream):
+def _ij_bboxes_launch(x_image, y_image, xy_bboxes, xy_border, grid, device, stream, fill=None):
     """Launch K4; returns (device int32 accumulators (n, 4), n, (w, h), grid
-    mode used)."""
+    mode used).  ``fill``: a contiguous 4-byte tensor K4's grid sets to ~0
+    (the claim-key scratch of the K5 call that follows, xrs_ij_bboxes_fill)."""
     device = require_device(device if device is not None else getattr(x_image, "device", None))
     x = to_device(x_image, device, np.float64)
     y = to_device(y_image, device, np.float64)
@@ -176,25 +177,37 @@ def _ij_bboxes_launch(x_image, y_image, xy_bboxes, xy_border, grid, device, stre
     if grid is not None:
         ntx, nty = grid
         bb = b.reshape(nty, ntx, 4)
-        if ntx * nty == n and np.all(bb[:, :, [0, 2]] == bb[:1, :, [0, 2]]) and \
-                np.all(bb[:, :, [1, 3]] == bb[:, :1, [1, 3]]):
-            bx = _upload_small(bb[0, :, [0, 2]].T, device, stream)
-            by = _upload_small(bb[:, 0, [1, 3]], device, stream)
-        else:
+        if not (ntx * nty == n and np.all(bb[:, :, [0, 2]] == bb[:1, :, [0, 2]]) and
+                np.all(bb[:, :, [1, 3]] == bb[:, :1, [1, 3]])):
             ntx = nty = 0
-    if ntx == 0:
-        bx = _upload_small(b, device, stream)
-        by = bx
-    acc = _upload_small(np.tile(np.array([[2**31 - 1, 2**31 - 1, -1, -1]], np.int32), (n, 1)),
-                        device, stream)
-    rc = _native.lib().xrs_ij_bboxes(ptr(x), ptr(y), h, w, x.stride(0), n, ntx, nty, ptr(bx),
-                                     ptr(by), ptr(acc), stream_handle(device, stream))
+    # one upload for the boxes and the accumulators' initial values (each
+    # small copy is a blit of ~6 us on the stream ahead of K4): float64 box
+    # bounds first, the int32 (i_min, j_min, i_max, j_max) after them
+    if ntx > 0:
+        parts = [bb[0, :, [0, 2]].T.reshape(-1), bb[:, 0, [1, 3]].reshape(-1)]
+    else:
+        parts = [b.reshape(-1)]
+    acc0 = np.tile(np.array([[2**31 - 1, 2**31 - 1, -1, -1]], np.int32), (n, 1))
+    blob = np.concatenate([np.concatenate(parts).astype(np.float64).view(np.uint8),
+                           acc0.reshape(-1).view(np.uint8)])
+    dev_blob = _upload_small(blob, device, stream)
+    nbx = parts[0].size
+    nb = sum(p.size for p in parts)
+    bx = dev_blob[:8 * nbx].view(torch().float64)
+    by = dev_blob[8 * nbx:8 * nb].view(torch().float64) if ntx > 0 else bx
+    acc = dev_blob[8 * nb:].view(torch().int32).view(n, 4)
+    if fill is not None and (not fill.is_contiguous() or fill.element_size() != 4):
+        raise ValueError("fill must be a contiguous tensor of 4-byte words")
+    rc = _native.lib().xrs_ij_bboxes_fill(
+        ptr(x), ptr(y), h, w, x.stride(0), n, ntx, nty, ptr(bx), ptr(by), ptr(acc),
+        ptr(fill) if fill is not None else None, fill.numel() if fill is not None else 0,
+        stream_handle(device, stream))
     _native.check(rc, "xrs_ij_bboxes")
     if stream is not None:
         # made on the current stream, read (acc: written) by K4 on `stream`:
         # bx / by (and uploaded coordinates) are freed when this returns, so
         # keep their memory from the allocator until `stream` is past K4
-        for t in (x, y, bx, by, acc):
+        for t in (x, y, dev_blob) + ((fill,) if fill is not None else ()):
             t.record_stream(stream)
     return acc, n, (w, h), ntx > 0
 
@@ -225,16 +238,39 @@ def ij_bboxes(x_image, y_image, xy_bboxes, xy_border: float = 0.0, ij_border: in
     return out
 
 
+class DeviceTiles:
+    """rectify_tiles_device's result: the tile records (uint8 tensor of
+    TILE_INFO records) and chunk offsets (int64 tensor) on the device —
+    unpacks as ``tiles, offs`` — and the claim-key scratch K4 filled beside
+    them.  The scratch serves the first K5 call given these tiles (its claim
+    pass consumes the fill); later calls fill their own."""
+
+    __slots__ = ("tiles", "offs", "_keys")
+
+    def __init__(self, tiles, offs, keys):
+        self.tiles, self.offs, self._keys = tiles, offs, keys
+
+    def __iter__(self):
+        return iter((self.tiles, self.offs))
+
+    def take_keys(self, dst_h: int, dst_w: int):
+        """The pre-filled (dst_h, dst_w) key scratch, once; else None."""
+        k, self._keys = self._keys, None
+        return k if k is not None and tuple(k.shape) == (dst_h, dst_w) else None
+
+
 def rectify_tiles_device(x_image, y_image, target_xy_bboxes, xy_border: float, ij_border: int,
                          grid: tuple[int, int], tile_size: tuple[int, int],
                          dst_size: tuple[int, int], dst_xy_min_max: tuple, dst_res: tuple,
                          j_axis_up: bool, device=None, stream=None):
     """K4 + xrs_rectify_tiles: the per-tile records and chunk offsets of
     rectify.py:312-419 computed and left on the device (no host round trip).
-    Returns (tiles uint8 tensor of TILE_INFO records, chunk offsets int64
-    tensor), or None when the boxes are not a regular tile grid."""
+    Returns a DeviceTiles (K4 also fills the K5 claim-key scratch), or None
+    when the boxes are not a regular tile grid."""
+    dev = require_device(device if device is not None else getattr(x_image, "device", None))
+    keys = torch().empty((dst_size[1], dst_size[0]), dtype=torch().int32, device=dev)
     acc, n, (w, h), is_grid = _ij_bboxes_launch(x_image, y_image, target_xy_bboxes, xy_border,
-                                                grid, device, stream)
+                                                grid, device, stream, fill=keys)
     if not is_grid:
         return None
     device = acc.device
@@ -248,7 +284,7 @@ def rectify_tiles_device(x_image, y_image, target_xy_bboxes, xy_border: float, i
         float(dst_res[1]), int(bool(j_axis_up)), ptr(tiles), ptr(offs),
         stream_handle(device, stream))
     _native.check(rc, "xrs_rectify_tiles")
-    return tiles, offs
+    return DeviceTiles(tiles, offs, keys)
 
 
 def transform(transformer, x, y, grid: bool, device=None, stream=None):
@@ -292,6 +328,15 @@ def strip_counts(swin, shin):
     return (nqi + STRIP_W - 1) // STRIP_W * ((nqj + STRIP_H - 1) // STRIP_H)
 
 
+def _claim_keys(tiles, dst_h, dst_w, device):
+    """K5's claim-key scratch and keys_ready: the one K4 filled (DeviceTiles,
+    first use), else a fresh one the call fills."""
+    k = tiles.take_keys(dst_h, dst_w) if isinstance(tiles, DeviceTiles) else None
+    if k is not None and k.device == device:
+        return k, 1
+    return torch().empty((dst_h, dst_w), dtype=torch().int32, device=device), 0
+
+
 def _rect_inputs(x_image, y_image, tiles, device):
     """Device x/y images, tile records, chunk offsets and the strip count
     of a K5 call (host tiles get their offsets computed here)."""
@@ -326,7 +371,7 @@ def rectify_ij(x_image, y_image, tiles: np.ndarray, ntiles_x: int, dst_h: int, d
     device = require_device(device)
     x, y, t_dev, offs, ntiles, max_chunks = _rect_inputs(x_image, y_image, tiles, device)
     h, w = x.shape
-    keys = torch().empty((dst_h, dst_w), dtype=torch().int32, device=device)
+    keys, keys_ready = _claim_keys(tiles, dst_h, dst_w, device)
     ij = (torch().full((2, dst_h, dst_w), float("nan"), dtype=torch().float64, device=device)
           if init_nan else torch().empty((2, dst_h, dst_w), dtype=torch().float64, device=device))
     own_flags = flags is None
@@ -335,7 +380,8 @@ def rectify_ij(x_image, y_image, tiles: np.ndarray, ntiles_x: int, dst_h: int, d
     rc = _native.lib().xrs_rectify_ij(ptr(x), ptr(y), h, w, x.stride(0), ptr(t_dev), ntiles,
                                       ntiles_x, ptr(offs), max_chunks, dst_h, dst_w,
                                       float(x_scale), float(y_scale), float(uv_delta),
-                                      ptr(keys), ptr(ij), flags.ptr, stream_handle(device, stream))
+                                      ptr(keys), keys_ready, ptr(ij), flags.ptr,
+                                      stream_handle(device, stream))
     _native.check(rc, "xrs_rectify_ij")
     if own_flags:
         flags.raise_if_set("xrs_rectify_ij")
@@ -362,7 +408,7 @@ def rectify_ij_var(x_image, y_image, tiles, dst_h: int, dst_w: int, x_scale: flo
     x, y, t_dev, offs, ntiles, max_chunks = _rect_inputs(x_image, y_image, tiles, device)
     h, w = x.shape
     n, sh, sw = src.shape
-    keys = torch().empty((dst_h, dst_w), dtype=torch().int32, device=device)
+    keys, keys_ready = _claim_keys(tiles, dst_h, dst_w, device)
     ij = (torch().empty((2, dst_h, dst_w), dtype=torch().float64, device=device)
           if keep_ij else None)
     out = torch().empty((n, dst_h, dst_w), dtype=src.dtype, device=device)
@@ -371,7 +417,7 @@ def rectify_ij_var(x_image, y_image, tiles, dst_h: int, dst_w: int, x_scale: flo
         flags = ErrorFlags(device)
     rc = _native.lib().xrs_rectify_ij_var(
         ptr(x), ptr(y), h, w, x.stride(0), ptr(t_dev), ntiles, ptr(offs), max_chunks, dst_h,
-        dst_w, float(x_scale), float(y_scale), float(uv_delta), ptr(keys),
+        dst_w, float(x_scale), float(y_scale), float(uv_delta), ptr(keys), keys_ready,
         ptr(ij) if ij is not None else None, ptr(src), _native.DTYPE_CODES[_np_dtype(src)], n,
         sh, sw, src.stride(0), src.stride(1), ptr(out), out.stride(0), code, float(fill),
         flags.ptr, stream_handle(device, stream))
