@@ -641,9 +641,11 @@ constexpr double kMargin = 1e-9;
 // floors of the four corners' pixel coordinates (rectify.py:500-526); floor is
 // monotone, so the window comes from the extreme corners: two floors per axis,
 // taken by the reciprocal when clearly (relative margin) away from an integer,
-// else from the reference's per-corner divisions.  The lane then walks only
-// the pixels whose centres can be hit (trim_window: about half the window's
-// area; the cut-off pixels are misses of both triangles).
+// else from the reference's per-corner divisions.  The lane walks only the
+// pixels whose centres can be hit (trim_pad: about a third of the window's
+// area at config 4; the cut-off pixels are misses of both triangles).  Those
+// lie inside the window whenever the pad is small, so the floors are taken
+// only for windows the wave walks (or quads of many pixels).
 //
 // Tests.  Per triangle (A = p0 p1 p2, B = p3 p2 p1) the reference computes
 // nu = _fu(...), nv = _fv(...) (rectify.py:737-768), u = nu / det, v = nv /
@@ -815,26 +817,18 @@ __device__ inline uint3 walk_pair(const TriForms A, const TriForms B, int n, int
   return uint3{h_a, h_b, h_uns & ~(h_a | h_b)};
 }
 
-// Trim a quad's window [i0, i1] x [j0, j1] (floors of the corners' extreme
-// pixel units q, rectify.py:500-526) to the pixels whose centre i + 0.5 lies
-// within `pad` of [qx0, qx1] x [qy0, qy1].  A point the reference counts as a
-// hit has u, v >= -d, u + v <= 1 + 2d with d = |uv_delta| + its rounding
+// The trim pad of a quad's window (floors of the corners' extreme pixel
+// units q, rectify.py:500-526): only pixels whose centre i + 0.5 lies within
+// `pad` of [qx0, qx1] x [qy0, qy1] can be hit.  A point the reference counts
+// as a hit has u, v >= -d, u + v <= 1 + 2d with d = |uv_delta| + its rounding
 // (<= the form bound M <= kMaxFormMargin, checked by tri_setup for both
 // triangles before a trimmed window is used); such points lie within
 // 4 d (extent) of the triangle's bounding box, so pad = 8 d (W + H) plus an
 // absolute 1e-6 (the rounding of q itself) leaves a factor 2 to spare.
 // Pixels cut off are misses of both triangles.
-__device__ inline void trim_window(double qx0, double qx1, double qy0, double qy1, double d,
-                                   int32_t& i0, int32_t& i1, int32_t& j0, int32_t& j1) {
-  const double pad = 8.0 * d * ((qx1 - qx0) + (qy1 - qy0)) +
-                     1e-6 * (1.0 + fmax(fmax(fabs(qx0), fabs(qx1)), fmax(fabs(qy0), fabs(qy1))));
-  const double ci = ceil(qx0 - 0.5 - pad), fi = floor(qx1 - 0.5 + pad);
-  const double cj = ceil(qy0 - 0.5 - pad), fj = floor(qy1 - 0.5 + pad);
-  const int32_t a0 = i0, a1 = i1, b0 = j0, b1 = j1;
-  if (ci > a0) i0 = (int32_t)fmin(ci, (double)a1 + 1.0);
-  if (fi < a1) i1 = (int32_t)fmax(fi, (double)a0 - 1.0);
-  if (cj > b0) j0 = (int32_t)fmin(cj, (double)b1 + 1.0);
-  if (fj < b1) j1 = (int32_t)fmax(fj, (double)b0 - 1.0);
+__device__ inline double trim_pad(double qx0, double qx1, double qy0, double qy1, double d) {
+  return 8.0 * d * ((qx1 - qx0) + (qy1 - qy0)) +
+         1e-6 * (1.0 + fmax(fmax(fabs(qx0), fabs(qx1)), fmax(fabs(qy0), fabs(qy1))));
 }
 
 __device__ inline double dpp_next_f64(double v) {   // lane i <- lane i + 1 (lane 63: 0)
@@ -996,7 +990,6 @@ rectify_claim_kernel(RectArgs a) {
       uint32_t hit = 0, hit_b = 0, unsure = 0;   // bit k: window pixel k (row-major) hit
                                                   // (hit_b: by triangle B) / undecided
       if (has_q) {
-        double fx0, fx1, fy0, fy1;
         // floor is monotone and the reciprocal's error tiny: the extremes of the
         // coordinates give the extreme pixel units
         const double qx0 = qx(fmin(fmin(t0.x, t1.x), fmin(b0.x, b1.x)));
@@ -1007,52 +1000,81 @@ rectify_claim_kernel(RectArgs a) {
         const double qy1 = qy(YPOS ? yhi : ylo);
         const double fin = t0.x + t1.x + b0.x + b1.x + t0.y + t1.y + b0.y + b1.y;
         if (fin - fin == 0.0 && fmax(fabs(qx0), fabs(qx1)) < 0x1p40 &&
-            fmax(fabs(qy0), fabs(qy1)) < 0x1p40 && floor_clear(qx0, a.margin, fx0) &&
-            floor_clear(qx1, a.margin, fx1) && floor_clear(qy0, a.margin, fy0) &&
-            floor_clear(qy1, a.margin, fy1)) {
-          int32_t i0 = (int32_t)fx0, i1 = (int32_t)fx1, j0 = (int32_t)fy0, j1 = (int32_t)fy1;
-          if (!(i1 < 0 || j1 < 0 || i0 >= ti.tw || j0 >= ti.th)) {
-            i0 = max(i0, 0); j0 = max(j0, 0);
-            i1 = min(i1, ti.tw - 1); j1 = min(j1, ti.th - 1);
-            const int64_t cnt_full = (int64_t)(i1 - i0 + 1) * (j1 - j0 + 1);
-            // pixel centres (i + 0.5) farther than `pad` from the corners'
-            // extremes are misses of both triangles (trim_window)
-            int32_t ti0 = i0, ti1 = i1, tj0 = j0, tj1 = j1;
-            trim_window(qx0, qx1, qy0, qy1, fabs(a.uv_delta) + kMaxFormMargin * a.margin_scale,
-                        ti0, ti1, tj0, tj1);
-            const int64_t cnt = (int64_t)(ti1 - ti0 + 1) * (tj1 - tj0 + 1);
-            if (ti0 > ti1 || tj0 > tj1) {
-              // no pixel centre near the quad: nothing to test
-            } else if (cnt > kLaneWindow) {
-              imin = i0; jmin = j0; nw = i1 - i0 + 1;   // untrimmed: exact test everywhere
-              big_cnt = cnt_full;   // (a quad without a triangle is dropped there)
-            } else {
-              imin = ti0; jmin = tj0;
-              nw = ti1 - ti0 + 1;
-              const int32_t nh = tj1 - tj0 + 1;
-              const int32_t n = (int32_t)cnt;
-              const double dx0 = ti.x_off + ((double)imin + 0.5) * a.x_scale;   // pixel (imin, jmin)
-              const double dy0 = ti.y_off + ((double)jmin + 0.5) * a.y_scale;
-              const float X = fabsf((float)ti.x_off) + (float)(ti.tw + 1) * fabsf((float)a.x_scale);
-              const float Y = fabsf((float)ti.y_off) + (float)(ti.th + 1) * fabsf((float)a.y_scale);
-              const float wn = (float)(nw - 1), hn = (float)(nh - 1);
-              // A = (p0, p1, p2): _fu(p, p0, p2), _fv(p, p0, p1), _fdet(p0, p1, p2)
-              // B = (p3, p2, p1): _fu(p, p3, p1), _fv(p, p3, p2), _fdet(p3, p2, p1)
-              int sa, sb;
-              const TriForms FA = tri_forms(t0.x - dx0, t0.y - dy0, t0.y - b0.y, t0.x - b0.x,
-                                            t0.x - t1.x, t0.y - t1.y, t0.x, t0.y, a, X, Y, wn,
-                                            hn, (float)umin, (float)uvmax, sa);
-              const TriForms FB = tri_forms(b1.x - dx0, b1.y - dy0, b1.y - t1.y, b1.x - t1.x,
-                                            b1.x - b0.x, b1.y - b0.y, b1.x, b1.y, a, X, Y, wn,
-                                            hn, (float)umin, (float)uvmax, sb);
-              if (sa < 0 || sb < 0) {
-                slow = true;   // a triangle without a usable bound: exact, untrimmed window
-              } else if (sa | sb) {
-                const uint3 m = walk_pair(FA, FB, n, nw);
-                hit = m.x | m.y;
-                hit_b = m.y;
-                unsure = m.z;
+            fmax(fabs(qy0), fabs(qy1)) < 0x1p40) {
+          // T: the pixel centres (i + 0.5) within `pad` of the corners'
+          // extremes, clipped to the tile — every other pixel is a miss of
+          // both triangles (trim_pad).  With pad + the reciprocal's error
+          // < 0.5, T lies inside the reference's window R = [floor(qx0),
+          // floor(qx1)] x [floor(qy0), floor(qy1)] (ceil(q - 0.5 - pad) >=
+          // floor(q) and floor(q - 0.5 + pad) <= floor(q)), so R — its exact
+          // floors — is needed only for the wave-wide walk of a large window
+          // (R untrimmed) or a quad so large that pad >= 0.25.
+          const double d = fabs(a.uv_delta) + kMaxFormMargin * a.margin_scale;
+          const double pad = trim_pad(qx0, qx1, qy0, qy1, d);
+          const double ci = ceil(qx0 - 0.5 - pad), fi = floor(qx1 - 0.5 + pad);
+          const double cj = ceil(qy0 - 0.5 - pad), fj = floor(qy1 - 0.5 + pad);
+          bool empty = !(ci <= fi && cj <= fj && fi >= 0.0 && fj >= 0.0 &&
+                         ci <= (double)(ti.tw - 1) && cj <= (double)(ti.th - 1));
+          int32_t ti0 = 0, ti1 = -1, tj0 = 0, tj1 = -1;
+          if (!empty) {
+            ti0 = (int32_t)fmax(ci, 0.0); ti1 = (int32_t)fmin(fi, (double)(ti.tw - 1));
+            tj0 = (int32_t)fmax(cj, 0.0); tj1 = (int32_t)fmin(fj, (double)(ti.th - 1));
+          }
+          int64_t cnt = (int64_t)(ti1 - ti0 + 1) * (tj1 - tj0 + 1);
+          bool walk = !empty;
+          // (the exact-decision test knob sets an infinite margin: R always)
+          if (pad >= 0.25 || !(a.margin < 0.25) || (!empty && cnt > kLaneWindow)) {
+            walk = false;
+            double fx0, fx1, fy0, fy1;
+            if (floor_clear(qx0, a.margin, fx0) && floor_clear(qx1, a.margin, fx1) &&
+                floor_clear(qy0, a.margin, fy0) && floor_clear(qy1, a.margin, fy1)) {
+              int32_t i0 = (int32_t)fx0, i1 = (int32_t)fx1, j0 = (int32_t)fy0, j1 = (int32_t)fy1;
+              if (!empty && !(i1 < 0 || j1 < 0 || i0 >= ti.tw || j0 >= ti.th)) {
+                i0 = max(i0, 0); j0 = max(j0, 0);
+                i1 = min(i1, ti.tw - 1); j1 = min(j1, ti.th - 1);
+                ti0 = max(ti0, i0); ti1 = min(ti1, i1);   // T inside R
+                tj0 = max(tj0, j0); tj1 = min(tj1, j1);
+                cnt = (int64_t)(ti1 - ti0 + 1) * (tj1 - tj0 + 1);
+                if (ti0 > ti1 || tj0 > tj1) {
+                  // no pixel centre near the quad: nothing to test
+                } else if (cnt > kLaneWindow) {
+                  imin = i0; jmin = j0; nw = i1 - i0 + 1;   // untrimmed: exact test everywhere
+                  big_cnt = (int64_t)(i1 - i0 + 1) * (j1 - j0 + 1);   // (a quad without a
+                                                                       // triangle is dropped there)
+                } else {
+                  walk = true;
+                }
               }
+            } else {
+              slow = true;
+            }
+          }
+          if (walk) {
+            imin = ti0; jmin = tj0;
+            nw = ti1 - ti0 + 1;
+            const int32_t nh = tj1 - tj0 + 1;
+            const int32_t n = (int32_t)cnt;
+            const double dx0 = ti.x_off + ((double)imin + 0.5) * a.x_scale;   // pixel (imin, jmin)
+            const double dy0 = ti.y_off + ((double)jmin + 0.5) * a.y_scale;
+            const float X = fabsf((float)ti.x_off) + (float)(ti.tw + 1) * fabsf((float)a.x_scale);
+            const float Y = fabsf((float)ti.y_off) + (float)(ti.th + 1) * fabsf((float)a.y_scale);
+            const float wn = (float)(nw - 1), hn = (float)(nh - 1);
+            // A = (p0, p1, p2): _fu(p, p0, p2), _fv(p, p0, p1), _fdet(p0, p1, p2)
+            // B = (p3, p2, p1): _fu(p, p3, p1), _fv(p, p3, p2), _fdet(p3, p2, p1)
+            int sa, sb;
+            const TriForms FA = tri_forms(t0.x - dx0, t0.y - dy0, t0.y - b0.y, t0.x - b0.x,
+                                          t0.x - t1.x, t0.y - t1.y, t0.x, t0.y, a, X, Y, wn,
+                                          hn, (float)umin, (float)uvmax, sa);
+            const TriForms FB = tri_forms(b1.x - dx0, b1.y - dy0, b1.y - t1.y, b1.x - t1.x,
+                                          b1.x - b0.x, b1.y - b0.y, b1.x, b1.y, a, X, Y, wn,
+                                          hn, (float)umin, (float)uvmax, sb);
+            if (sa < 0 || sb < 0) {
+              slow = true;   // a triangle without a usable bound: exact, untrimmed window
+            } else if (sa | sb) {
+              const uint3 m = walk_pair(FA, FB, n, nw);
+              hit = m.x | m.y;
+              hit_b = m.y;
+              unsure = m.z;
             }
           }
         } else {
