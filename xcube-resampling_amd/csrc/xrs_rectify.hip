@@ -655,7 +655,7 @@ constexpr double kMargin = 1e-9;
 // forms of both triangles in float32 (two FMAs each), shifted so that a hit is
 // min3(u', v', s') >= 0, with a per-quad bound M on |form - the reference's
 // float64 value| (float32 evaluation + conversion of the coefficients, plus
-// the reference's own rounding of dx, ex, nu, u: LinQuad::setup).  A pixel is
+// the reference's own rounding of dx, ex, nu, u: TriForms2).  A pixel is
 // decided by the forms when max over the triangles of min3 is >= 0 (some
 // triangle surely hits) or < -2M (every triangle surely misses), else — a
 // pixel centre within M of a triangle edge, rare — by the reference's exact
@@ -677,57 +677,6 @@ constexpr int kLaneWindow = 16;  // windows up to this many pixels: walked per l
 constexpr double kEps64 = 0x1p-52;
 constexpr double kEps32 = 0x1p-23;
 constexpr double kMaxFormMargin = 1e-3;   // larger bound: exact test at every pixel
-
-// One triangle's three affine forms over the quad's pixel window (float32)
-// and the decision threshold thr = -2M.  form(a, b) = c0 + a ci + b cj.
-struct TriForms {
-  // (c0, ci, cj) of u - umin - M, v - umin - M, uvmax - M - (u + v); named
-  // members, not an array: an array of these (read as overlapping float
-  // pairs by the packed walk) was kept in memory — the compiler put it in
-  // LDS, one 40-byte slot per lane, with bank conflicts on every read
-  float u0, ui, uj, v0, vi, vj, w0, wi, wj;
-  float thr;
-};
-
-// One triangle's forms over the window, evaluated in float32 (window position
-// (0, 0) = the pixel centre at which the corner differences (ex, ey) are
-// taken, in float64 exactly as the reference takes them).  e1..e4: the edge
-// factors of _fu(p, c, q) = ex e1 - ey e2 and _fv(p, c, r) = ey e3 - ex e4
-// (rectify.py:745-768); det = _fdet(...) != 0; the pixel centre moves by
-// (sx, sy) per column / row (ex -= sx, ey -= sy).  M bounds |form - the
-// reference's float64 value| over the window:
-//   float32: the inputs rounded to float (ex, ey, e, det), the reciprocal
-//     (1 ulp), the products and sums of u0, v0 (terms pu, pv), of the steps,
-//     and the two FMAs over the window (T, g): <= E eps32, with a factor >= 2
-//     to spare in every term
-//   reference: dx = x_off + (i + 0.5) sx and ex = x0 - dx round by
-//     <= eps64 (3 X + |x0|), X = |x_off| + (tw + 1) |sx|; the products of nu
-//     by eps64 |ex e|; u = nu / det by eps64 |u|: <= 5 eps64 R + eps64 T
-// M = 2 (E eps32 + 10 eps64 R + 8 eps64 T), evaluated in float32 and scaled
-// up by 1.01 for its own rounding.  Returns false (every pixel of the window
-// to the exact test) when M is NaN / inf or above kMaxFormMargin (degenerate
-// triangles).
-__device__ inline TriForms tri_setup(double ex64, double ey64, double e1_64, double e2_64,
-                                     double e3_64, double e4_64, double det, float sx, float sy,
-                                     float X, float Y, float ax, float ay, float wn, float hn,
-                                     float umin, float uvmax, float margin_scale, bool& ok) {
-  const float ex = (float)ex64, ey = (float)ey64;
-  const float e1 = (float)e1_64, e2 = (float)e2_64, e3 = (float)e3_64, e4 = (float)e4_64;
-  const float r = __builtin_amdgcn_rcpf((float)det), ar = fabsf(r);
-  const float pu = (fabsf(ex * e1) + fabsf(ey * e2)) * ar;   // |terms| of u0
-  const float pv = (fabsf(ey * e3) + fabsf(ex * e4)) * ar;
-  const float u0 = (ex * e1 - ey * e2) * r, v0 = (ey * e3 - ex * e4) * r;
-  const float ui = -sx * e1 * r, uj = sy * e2 * r, vi = sx * e4 * r, vj = -sy * e3 * r;
-  const float g = wn * (fabsf(ui) + fabsf(vi)) + hn * (fabsf(uj) + fabsf(vj));
-  const float T = fabsf(u0) + fabsf(v0) + g;
-  const float E = 10.0f * (pu + pv) + 8.0f * g + 6.0f * (T + 4.0f);
-  const float R = ((X + ax) * (fabsf(e1) + fabsf(e4)) + (Y + ay) * (fabsf(e2) + fabsf(e3))) * ar;
-  const float M = 2.02f * ((float)kEps32 * E + 10.0f * (float)kEps64 * R +
-                           8.0f * (float)kEps64 * T) * margin_scale;
-  ok = M <= (float)kMaxFormMargin * margin_scale;
-  return TriForms{(u0 - umin) - M, ui, uj, (v0 - umin) - M, vi, vj,
-                  (uvmax - (u0 + v0)) - M, -(ui + vi), -(uj + vj), -2.0f * M};
-}
 
 // the reference's test of one triangle at pixel centre (dx, dy)
 // (rectify.py:556-573): A = (p0; p2, p1), B = (p3; p1, p2)
@@ -761,33 +710,91 @@ __device__ inline uint32_t claim_key(const RectArgs& a, uint32_t key, int tri) {
   return a.tri_bit ? (key << 1) | (uint32_t)(tri - 1) : key;
 }
 
-// One triangle's forms for the pair walk: 1 = forms set up, 0 = no triangle
-// (_fdet NaN or 0: never hits; forms that are -inf everywhere), -1 = no usable
-// bound (the lane takes the reference's test over the untrimmed window).
-// (returned by value, status in `st`: the forms stay in registers)
-__device__ inline TriForms tri_forms(double ex, double ey, double e1, double e2, double e3,
-                                     double e4, double cx, double cy, const RectArgs& a,
-                                     float X, float Y, float wn, float hn, float umin,
-                                     float uvmax, int& st) {
-  const double det = e3 * e1 - e2 * e4;   // _fdet from the edge factors
-  if (det != det || det == 0.0) {
-    st = 0;
-    return TriForms{-INFINITY, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
-  }
-  bool ok;
-  const TriForms F = tri_setup(ex, ey, e1, e2, e3, e4, det, (float)a.x_scale, (float)a.y_scale,
-                               X, Y, fabsf((float)cx), fabsf((float)cy), wn, hn, umin, uvmax,
-                               a.margin_scale, ok);
-  st = ok ? 1 : -1;
-  return F;
-}
-
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
-__device__ inline f32x2 form2(float a0, float ai, float aj, float b0, float bi, float bj,
-                              f32x2 av, f32x2 bv) {
-  const f32x2 c0 = {a0, b0}, ci = {ai, bi}, cj = {aj, bj};
-  return __builtin_elementwise_fma(bv, cj, __builtin_elementwise_fma(av, ci, c0));
+// The three affine forms of both triangles over the quad's pixel window
+// (float32; A in .x, B in .y: one packed v_pk_* instruction for the pair) and
+// the decision threshold thr = -2M.  form(a, b) = c0 + a ci + b cj; (c0, ci,
+// cj) of u - umin - M, v - umin - M, uvmax - M - (u + v).  Named members, not
+// an array: an array of forms (read as overlapping float pairs by the packed
+// walk) was kept in memory — the compiler put it in LDS, one 40-byte slot per
+// lane, with bank conflicts on every read.
+//
+// Window position (0, 0) = the pixel centre at which the corner differences
+// (ex, ey) are taken, in float64 exactly as the reference takes them.
+// e1..e4: the edge factors of _fu(p, c, q) = ex e1 - ey e2 and _fv(p, c, r) =
+// ey e3 - ex e4 (rectify.py:745-768); det = _fdet(...) != 0, r = 1 / det; the
+// pixel centre moves by (sx, sy) per column / row (ex -= sx, ey -= sy).
+// M bounds |form - the reference's float64 value| over the window:
+//   float32: the inputs rounded to float (ex, ey, e, det), the reciprocal
+//     (1 ulp), the products and sums of u0, v0 (terms pu = (|ex e1| + |ey e2|)
+//     |r|, pv likewise), of the steps, and the two FMAs over the window
+//     (T = |u0| + |v0| + g, g = wn (|ui| + |vi|) + hn (|uj| + |vj|)):
+//     <= E eps32, E = 10 (pu + pv) + 8 g + 6 (T + 4), a factor >= 2 to spare
+//     in every term
+//   reference: dx = x_off + (i + 0.5) sx and ex = x0 - dx round by
+//     <= eps64 (3 X + |x0|), X = |x_off| + (tw + 1) |sx|; the products of nu
+//     by eps64 |ex e|; u = nu / det by eps64 |u|: <= 5 eps64 R + eps64 T,
+//     R = ((X + |x0|) (|e1| + |e4|) + (Y + |y0|) (|e2| + |e3|)) |r|
+// M = 2 (E eps32 + 10 eps64 R + 8 eps64 T), scaled up by 1.01 for its own
+// float32 rounding, each magnitude taken by a simpler upper bound (a larger M
+// sends more pixels to the exact test, never fewer): with S = |e1| + |e2| +
+// |e3| + |e4|, Sr = S |r|: pu + pv <= (|ex| + |ey|) Sr = P, |u0| + |v0| <= P,
+// g <= max(wn |sx|, hn |sy|) Sr = G, T <= P + G, E <= 16 P + 14 G + 24,
+// R <= (2 max(X, Y) + |ex| + |ey|) Sr (a corner's |x0| <= |ex| + |dx0| and
+// |dx0| <= X).  A triangle whose M is NaN / inf or above kMaxFormMargin
+// (degenerate) sends every pixel of the window to the exact test.
+struct TriForms2 {
+  f32x2 u0, ui, uj, v0, vi, vj, w0, wi, wj;
+  f32x2 thr;
+};
+
+// Status st.x / st.y per triangle: 1 = forms set up, 0 = no triangle (_fdet
+// NaN or 0: never hits; forms -inf everywhere), -1 = no usable bound (the
+// lane takes the reference's test over the untrimmed window).  Returned by
+// value: the forms stay in registers.
+__device__ inline TriForms2 tri_forms2(const double (&ex)[2], const double (&ey)[2],
+                                       const double (&e1)[2], const double (&e2)[2],
+                                       const double (&e3)[2], const double (&e4)[2],
+                                       float sx, float sy, float XY2, float G0, float umin,
+                                       float uvmax, float margin_scale, int2& st) {
+  f32x2 fex, fey, f1, f2, f3, f4, fr, fS, fxy;
+  bool tri[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const double det = e3[t] * e1[t] - e2[t] * e4[t];   // _fdet from the edge factors
+    tri[t] = !(det != det || det == 0.0);
+    fex[t] = (float)ex[t]; fey[t] = (float)ey[t];
+    f1[t] = (float)e1[t]; f2[t] = (float)e2[t]; f3[t] = (float)e3[t]; f4[t] = (float)e4[t];
+    fr[t] = __builtin_amdgcn_rcpf((float)det);
+    fS[t] = (float)((fabs(e1[t]) + fabs(e2[t])) + (fabs(e3[t]) + fabs(e4[t])));
+    fxy[t] = (float)(fabs(ex[t]) + fabs(ey[t]));
+  }
+  const f32x2 u0 = (fex * f1 - fey * f2) * fr, v0 = (fey * f3 - fex * f4) * fr;
+  const f32x2 sxr = sx * fr, syr = sy * fr;
+  const f32x2 ui = -(sxr * f1), uj = syr * f2, vi = sxr * f4, vj = -(syr * f3);
+  const f32x2 Sr = fS * __builtin_elementwise_abs(fr);
+  const f32x2 P = fxy * Sr, G = G0 * Sr;
+  const f32x2 T = P + G;
+  const f32x2 E = 16.0f * P + (14.0f * G + 24.0f);
+  const f32x2 R = (XY2 + fxy) * Sr;
+  const f32x2 M = ((float)kEps32 * E + (float)kEps64 * (10.0f * R + 8.0f * T)) *
+                  (2.02f * margin_scale);
+  TriForms2 F{(u0 - umin) - M, ui, uj, (v0 - umin) - M, vi, vj,
+              (uvmax - (u0 + v0)) - M, -(ui + vi), -(uj + vj), -2.0f * M};
+  int sts[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    sts[t] = !tri[t] ? 0 : (M[t] <= (float)kMaxFormMargin * margin_scale ? 1 : -1);
+    if (!tri[t]) {   // never hits: forms -inf everywhere
+      F.u0[t] = -INFINITY; F.ui[t] = F.uj[t] = 0.0f;
+      F.v0[t] = F.vi[t] = F.vj[t] = 0.0f;
+      F.w0[t] = F.wi[t] = F.wj[t] = 0.0f;
+      F.thr[t] = 0.0f;
+    }
+  }
+  st = int2{sts[0], sts[1]};
+  return F;
 }
 
 // Walk the window's n pixels (row-major, nw per row) for both triangles at
@@ -796,21 +803,21 @@ __device__ inline f32x2 form2(float a0, float ai, float aj, float b0, float bi, 
 // reference tests A first, so a pixel is A's when A surely hits (min3 >= 0),
 // B's when B surely hits and A surely misses (min3 < -2M); any other pixel
 // with some min3 >= -2M takes the exact tests.
-__device__ inline uint3 walk_pair(const TriForms A, const TriForms B, int n, int nw) {
+__device__ inline uint3 walk_pair(const TriForms2& F, int n, int nw) {
   uint32_t h_a = 0, h_b = 0, h_uns = 0;
   float af = 0.0f, bf = 0.0f;
   int col = 0;
   for (int k = 0; k < n; ++k) {
     const f32x2 av = {af, af}, bv = {bf, bf};
-    const f32x2 u = form2(A.u0, A.ui, A.uj, B.u0, B.ui, B.uj, av, bv);
-    const f32x2 v = form2(A.v0, A.vi, A.vj, B.v0, B.vi, B.vj, av, bv);
-    const f32x2 w = form2(A.w0, A.wi, A.wj, B.w0, B.wi, B.wj, av, bv);
+    const f32x2 u = __builtin_elementwise_fma(bv, F.uj, __builtin_elementwise_fma(av, F.ui, F.u0));
+    const f32x2 v = __builtin_elementwise_fma(bv, F.vj, __builtin_elementwise_fma(av, F.vi, F.v0));
+    const f32x2 w = __builtin_elementwise_fma(bv, F.wj, __builtin_elementwise_fma(av, F.wi, F.w0));
     const float ha = fminf(u.x, fminf(v.x, w.x)), hb = fminf(u.y, fminf(v.y, w.y));
     const uint32_t bit = 1u << k;
-    const bool a_in = ha >= 0.0f, a_near = ha >= A.thr;
+    const bool a_in = ha >= 0.0f, a_near = ha >= F.thr.x;
     h_a |= a_in ? bit : 0u;
     h_b |= (hb >= 0.0f && !a_near) ? bit : 0u;
-    h_uns |= (a_near || hb >= B.thr) ? bit : 0u;
+    h_uns |= (a_near || hb >= F.thr.y) ? bit : 0u;
     af += 1.0f;
     if (++col == nw) { col = 0; af = 0.0f; bf += 1.0f; }
   }
@@ -821,7 +828,7 @@ __device__ inline uint3 walk_pair(const TriForms A, const TriForms B, int n, int
 // units q, rectify.py:500-526): only pixels whose centre i + 0.5 lies within
 // `pad` of [qx0, qx1] x [qy0, qy1] can be hit.  A point the reference counts
 // as a hit has u, v >= -d, u + v <= 1 + 2d with d = |uv_delta| + its rounding
-// (<= the form bound M <= kMaxFormMargin, checked by tri_setup for both
+// (<= the form bound M <= kMaxFormMargin, checked by tri_forms2 for both
 // triangles before a trimmed window is used); such points lie within
 // 4 d (extent) of the triangle's bounding box, so pad = 8 d (W + H) plus an
 // absolute 1e-6 (the rounding of q itself) leaves a factor 2 to spare.
@@ -913,7 +920,7 @@ __device__ inline void claim_exact_lane(const RectArgs& a, const TileInfo& ti, i
 // HBM; YPOS: the sign of y_scale (j axis up), which decides whether the
 // corners' min or max y gives the first window row — a launch constant
 template <bool LDS_OFFS, bool YPOS>
-__global__ void __launch_bounds__(kClaimThreads)
+__global__ void __launch_bounds__(kClaimThreads, 4)   // <= 128 VGPRs: 4 waves per SIMD
 rectify_claim_kernel(RectArgs a) {
   __shared__ int64_t offs_s[kClaimOffsLds + 1];
   const int lane = threadIdx.x & 63;
@@ -949,6 +956,11 @@ rectify_claim_kernel(RectArgs a) {
       continue;
     }
     const int32_t nq_i = ti.swin - 1, nq_j = ti.shin - 1;
+    // form bound constants of the tile (tri_forms2): 2 max(X, Y) with X =
+    // |x_off| + (tw + 1) |sx| bounding a pixel centre's |x| (Y likewise)
+    const float sxf = (float)a.x_scale, syf = (float)a.y_scale;
+    const float XY2 = 2.0f * fmaxf(fabsf((float)ti.x_off) + (float)(ti.tw + 1) * fabsf(sxf),
+                                   fabsf((float)ti.y_off) + (float)(ti.th + 1) * fabsf(syf));
     const int32_t ncx = (nq_i + kStripW - 1) / kStripW;
     const int32_t cc = (int32_t)(c - off_lo);
     const int32_t cy = cc / ncx, cx = cc - cy * ncx;
@@ -1056,22 +1068,20 @@ rectify_claim_kernel(RectArgs a) {
             const int32_t n = (int32_t)cnt;
             const double dx0 = ti.x_off + ((double)imin + 0.5) * a.x_scale;   // pixel (imin, jmin)
             const double dy0 = ti.y_off + ((double)jmin + 0.5) * a.y_scale;
-            const float X = fabsf((float)ti.x_off) + (float)(ti.tw + 1) * fabsf((float)a.x_scale);
-            const float Y = fabsf((float)ti.y_off) + (float)(ti.th + 1) * fabsf((float)a.y_scale);
             const float wn = (float)(nw - 1), hn = (float)(nh - 1);
             // A = (p0, p1, p2): _fu(p, p0, p2), _fv(p, p0, p1), _fdet(p0, p1, p2)
             // B = (p3, p2, p1): _fu(p, p3, p1), _fv(p, p3, p2), _fdet(p3, p2, p1)
-            int sa, sb;
-            const TriForms FA = tri_forms(t0.x - dx0, t0.y - dy0, t0.y - b0.y, t0.x - b0.x,
-                                          t0.x - t1.x, t0.y - t1.y, t0.x, t0.y, a, X, Y, wn,
-                                          hn, (float)umin, (float)uvmax, sa);
-            const TriForms FB = tri_forms(b1.x - dx0, b1.y - dy0, b1.y - t1.y, b1.x - t1.x,
-                                          b1.x - b0.x, b1.y - b0.y, b1.x, b1.y, a, X, Y, wn,
-                                          hn, (float)umin, (float)uvmax, sb);
-            if (sa < 0 || sb < 0) {
+            const double ex[2] = {t0.x - dx0, b1.x - dx0}, ey[2] = {t0.y - dy0, b1.y - dy0};
+            const double e1[2] = {t0.y - b0.y, b1.y - t1.y}, e2[2] = {t0.x - b0.x, b1.x - t1.x};
+            const double e3[2] = {t0.x - t1.x, b1.x - b0.x}, e4[2] = {t0.y - t1.y, b1.y - b0.y};
+            int2 st;
+            const TriForms2 F = tri_forms2(ex, ey, e1, e2, e3, e4, sxf, syf, XY2,
+                                           fmaxf(wn * fabsf(sxf), hn * fabsf(syf)), (float)umin,
+                                           (float)uvmax, a.margin_scale, st);
+            if (st.x < 0 || st.y < 0) {
               slow = true;   // a triangle without a usable bound: exact, untrimmed window
-            } else if (sa | sb) {
-              const uint3 m = walk_pair(FA, FB, n, nw);
+            } else if (st.x | st.y) {
+              const uint3 m = walk_pair(F, n, nw);
               hit = m.x | m.y;
               hit_b = m.y;
               unsure = m.z;
