@@ -799,29 +799,31 @@ __device__ inline TriForms2 tri_forms2(const double (&ex)[2], const double (&ey)
 
 // Walk the window's n pixels (row-major, nw per row) for both triangles at
 // once: triangle A in the low and B in the high half of packed float32 FMAs
-// (v_pk_fma_f32).  Returns bit masks (hit by A, hit by B, undecided): the
-// reference tests A first, so a pixel is A's when A surely hits (min3 >= 0),
-// B's when B surely hits and A surely misses (min3 < -2M); any other pixel
-// with some min3 >= -2M takes the exact tests.
-__device__ inline uint3 walk_pair(const TriForms2& F, int n, int nw) {
-  uint32_t h_a = 0, h_b = 0, h_uns = 0;
+// (v_pk_fma_f32).  Returns a 2-bit code per pixel k at bits 2k, 2k + 1: 1 =
+// A's (A surely hits, min3 >= 0), 2 = B's (B surely hits and A surely misses,
+// min3 < -2M — the reference tests A first), 3 = undecided (some min3 >=
+// -2M otherwise: the exact tests), 0 = miss.  One code word instead of three
+// masks, and the column / row stepped in float (wn = nw - 1): fewer
+// instructions per pixel.
+__device__ inline uint32_t walk_pair(const TriForms2& F, int n, float wn) {
+  uint32_t W = 0;
   float af = 0.0f, bf = 0.0f;
-  int col = 0;
   for (int k = 0; k < n; ++k) {
     const f32x2 av = {af, af}, bv = {bf, bf};
     const f32x2 u = __builtin_elementwise_fma(bv, F.uj, __builtin_elementwise_fma(av, F.ui, F.u0));
     const f32x2 v = __builtin_elementwise_fma(bv, F.vj, __builtin_elementwise_fma(av, F.vi, F.v0));
     const f32x2 w = __builtin_elementwise_fma(bv, F.wj, __builtin_elementwise_fma(av, F.wi, F.w0));
     const float ha = fminf(u.x, fminf(v.x, w.x)), hb = fminf(u.y, fminf(v.y, w.y));
-    const uint32_t bit = 1u << k;
     const bool a_in = ha >= 0.0f, a_near = ha >= F.thr.x;
-    h_a |= a_in ? bit : 0u;
-    h_b |= (hb >= 0.0f && !a_near) ? bit : 0u;
-    h_uns |= (a_near || hb >= F.thr.y) ? bit : 0u;
-    af += 1.0f;
-    if (++col == nw) { col = 0; af = 0.0f; bf += 1.0f; }
+    const uint32_t c = a_in ? 1u
+                     : (!a_near && hb >= 0.0f) ? 2u
+                     : (a_near || hb >= F.thr.y) ? 3u : 0u;
+    W |= c << (2 * k);
+    const bool wrap = af == wn;
+    af = wrap ? 0.0f : af + 1.0f;
+    bf = wrap ? bf + 1.0f : bf;
   }
-  return uint3{h_a, h_b, h_uns & ~(h_a | h_b)};
+  return W;
 }
 
 // The trim pad of a quad's window (floors of the corners' extreme pixel
@@ -999,7 +1001,7 @@ rectify_claim_kernel(RectArgs a) {
       int32_t imin = 0, jmin = 0, nw = 0;
       int64_t big_cnt = 0;   // > 0: window above kLaneWindow, walked by the wave below
       bool slow = false;     // window not decided fast: claim_exact_lane
-      uint32_t hit = 0, hit_b = 0, unsure = 0;   // bit k: window pixel k (row-major) hit
+      uint32_t hit = 0, hit_b = 0, unsure = 0;   // bit 2k: window pixel k (row-major) hit
                                                   // (hit_b: by triangle B) / undecided
       if (has_q) {
         // floor is monotone and the reciprocal's error tiny: the extremes of the
@@ -1081,10 +1083,10 @@ rectify_claim_kernel(RectArgs a) {
             if (st.x < 0 || st.y < 0) {
               slow = true;   // a triangle without a usable bound: exact, untrimmed window
             } else if (st.x | st.y) {
-              const uint3 m = walk_pair(F, n, nw);
-              hit = m.x | m.y;
-              hit_b = m.y;
-              unsure = m.z;
+              const uint32_t W = walk_pair(F, n, wn);
+              hit = (W ^ (W >> 1)) & 0x55555555u;   // codes 1, 2 at bit 2k
+              hit_b = W >> 1;                        // bit 2k: the code's high bit
+              unsure = W & (W >> 1) & 0x55555555u;  // code 3
             }
           }
         } else {
@@ -1106,25 +1108,25 @@ rectify_claim_kernel(RectArgs a) {
           const uint32_t lbase = (uint32_t)jmin * w32 + (uint32_t)imin;
           const uint32_t lstride = w32 - (uint32_t)nw;
           while (hit) {
-            const int k = __builtin_ctz(hit);
+            const int k2 = __builtin_ctz(hit), k = k2 >> 1;
             hit &= hit - 1;
             const uint32_t dj = (uint32_t)(((float)k + 0.5f) * rnw);
             const uint32_t off = lbase + (uint32_t)k + __umul24(dj, lstride);
             atomicMin(reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(tile_keys) + (off << 2)),
-                      (hit_b >> k) & 1u ? key_b : key_a);
+                      (hit_b >> k2) & 1u ? key_b : key_a);
           }
         }
         while (hit) {
-          const int k = __builtin_ctz(hit);
+          const int k2 = __builtin_ctz(hit), k = k2 >> 1;
           hit &= hit - 1;
           const int32_t dj = (int32_t)(((float)k + 0.5f) * rnw);
           atomicMin(tile_keys + (int64_t)(jmin + dj) * a.dst_w + imin + k - dj * nw,
-                    (hit_b >> k) & 1u ? key_b : key_a);
+                    (hit_b >> k2) & 1u ? key_b : key_a);
         }
         if (unsure) {   // a pixel centre within the margin of an edge: the reference's test
           const Quad Q = load_quad(a, qj, qi);
           do {
-            const int k = __builtin_ctz(unsure);
+            const int k = __builtin_ctz(unsure) >> 1;
             unsure &= unsure - 1;
             const int32_t dj = (int32_t)(((float)k + 0.5f) * rnw);
             const int32_t di = imin + k - dj * nw;
