@@ -833,11 +833,11 @@ __device__ inline uint32_t walk_pair(const TriForms2& F, int n, float wn) {
 // (<= the form bound M <= kMaxFormMargin, checked by tri_forms2 for both
 // triangles before a trimmed window is used); such points lie within
 // 4 d (extent) of the triangle's bounding box, so pad = 8 d (W + H) plus an
-// absolute 1e-6 (the rounding of q itself) leaves a factor 2 to spare.
+// absolute 1e-6 (1 + max |q|) (the rounding of q itself) leaves a factor 2 to spare.
 // Pixels cut off are misses of both triangles.
-__device__ inline double trim_pad(double qx0, double qx1, double qy0, double qy1, double d) {
-  return 8.0 * d * ((qx1 - qx0) + (qy1 - qy0)) +
-         1e-6 * (1.0 + fmax(fmax(fabs(qx0), fabs(qx1)), fmax(fabs(qy0), fabs(qy1))));
+__device__ inline double trim_pad(double qx0, double qx1, double qy0, double qy1, double sq,
+                                  double d) {   // sq >= max |q|
+  return 8.0 * d * ((qx1 - qx0) + (qy1 - qy0)) + 1e-6 * (1.0 + sq);
 }
 
 __device__ inline double dpp_next_f64(double v) {   // lane i <- lane i + 1 (lane 63: 0)
@@ -849,6 +849,11 @@ __device__ inline double dpp_next_f64(double v) {   // lane i <- lane i + 1 (lan
 
 struct StripPoint {    // one source point of the strip
   double x, y;
+};
+
+struct PairExt {       // a point pair's coordinate extremes; both points finite
+  double xmn, xmx, ymn, ymx;
+  bool fin;
 };
 
 __device__ inline StripPoint strip_next(const StripPoint& p) {
@@ -989,14 +994,24 @@ rectify_claim_kernel(RectArgs a) {
     auto qx = [&](double x) { return (x - ti.x_off) * a.inv_x; };
     auto qy = [&](double y) { return (y - ti.y_off) * a.inv_y; };
     StripPoint t0 = load_pt(ti.sj0 + r0);
-    StripPoint t1 = strip_next(t0);
+    // a row's point pairs (l, l + 1): their extremes and finiteness sum, for
+    // the quads above and below the row (computed once, not per quad)
+    auto pair_ext = [](const StripPoint& p, const StripPoint& q) {
+      const double sum = (p.x + q.x) + (p.y + q.y);   // NaN / inf if any is
+      return PairExt{fmin(p.x, q.x), fmax(p.x, q.x), fmin(p.y, q.y), fmax(p.y, q.y),
+                     sum - sum == 0.0};
+    };
+    PairExt et = pair_ext(t0, strip_next(t0));
     StripPoint nxt = load_pt(ti.sj0 + r0 + 1);
     for (int32_t r = r0; r < r_end; ++r) {
       const int32_t qj = ti.sj0 + r;                    // global quad row (corner p0)
+      // (the top row's right-hand corners are re-shifted, not kept: registers)
+      const StripPoint t1 = strip_next(t0);
       const StripPoint b0 = nxt;
       // the next row's bottom points are requested before this row's tests
       if (r + 1 < r_end) nxt = load_pt(qj + 2);
       const StripPoint b1 = strip_next(b0);
+      const PairExt eb = pair_ext(b0, b1);
       // corners p0 = t0, p1 = t1, p2 = b0, p3 = b1
       int32_t imin = 0, jmin = 0, nw = 0;
       int64_t big_cnt = 0;   // > 0: window above kLaneWindow, walked by the wave below
@@ -1006,15 +1021,17 @@ rectify_claim_kernel(RectArgs a) {
       if (has_q) {
         // floor is monotone and the reciprocal's error tiny: the extremes of the
         // coordinates give the extreme pixel units
-        const double qx0 = qx(fmin(fmin(t0.x, t1.x), fmin(b0.x, b1.x)));
-        const double qx1 = qx(fmax(fmax(t0.x, t1.x), fmax(b0.x, b1.x)));
-        const double ylo = fmin(fmin(t0.y, t1.y), fmin(b0.y, b1.y));
-        const double yhi = fmax(fmax(t0.y, t1.y), fmax(b0.y, b1.y));
+        const double qx0 = qx(fmin(et.xmn, eb.xmn));
+        const double qx1 = qx(fmax(et.xmx, eb.xmx));
+        const double ylo = fmin(et.ymn, eb.ymn);
+        const double yhi = fmax(et.ymx, eb.ymx);
         const double qy0 = qy(YPOS ? ylo : yhi);
         const double qy1 = qy(YPOS ? yhi : ylo);
-        const double fin = t0.x + t1.x + b0.x + b1.x + t0.y + t1.y + b0.y + b1.y;
-        if (fin - fin == 0.0 && fmax(fabs(qx0), fabs(qx1)) < 0x1p40 &&
-            fmax(fabs(qy0), fabs(qy1)) < 0x1p40) {
+
+        // sq >= every |q| (a sum, not a max: no NaN-quieting of the operands);
+        // conditions combined with & (one branch, not one per term)
+        const double sq = (fabs(qx0) + fabs(qx1)) + (fabs(qy0) + fabs(qy1));
+        if (et.fin & eb.fin & (sq < 0x1p40)) {
           // T: the pixel centres (i + 0.5) within `pad` of the corners'
           // extremes, clipped to the tile — every other pixel is a miss of
           // both triangles (trim_pad).  With pad + the reciprocal's error
@@ -1024,15 +1041,19 @@ rectify_claim_kernel(RectArgs a) {
           // floors — is needed only for the wave-wide walk of a large window
           // (R untrimmed) or a quad so large that pad >= 0.25.
           const double d = fabs(a.uv_delta) + kMaxFormMargin * a.margin_scale;
-          const double pad = trim_pad(qx0, qx1, qy0, qy1, d);
-          const double ci = ceil(qx0 - 0.5 - pad), fi = floor(qx1 - 0.5 + pad);
-          const double cj = ceil(qy0 - 0.5 - pad), fj = floor(qy1 - 0.5 + pad);
-          bool empty = !(ci <= fi && cj <= fj && fi >= 0.0 && fj >= 0.0 &&
-                         ci <= (double)(ti.tw - 1) && cj <= (double)(ti.th - 1));
+          const double pad = trim_pad(qx0, qx1, qy0, qy1, sq, d);
+          const double lo = 0.5 + pad, hi = 0.5 - pad;
+          const double ci = ceil(qx0 - lo), fi = floor(qx1 - hi);
+          const double cj = ceil(qy0 - lo), fj = floor(qy1 - hi);
+          const double twm1 = (double)(ti.tw - 1), thm1 = (double)(ti.th - 1);
+          const bool empty = !((ci <= fi) & (cj <= fj) & (fi >= 0.0) & (fj >= 0.0) &
+                               (ci <= twm1) & (cj <= thm1));
           int32_t ti0 = 0, ti1 = -1, tj0 = 0, tj1 = -1;
-          if (!empty) {
-            ti0 = (int32_t)fmax(ci, 0.0); ti1 = (int32_t)fmin(fi, (double)(ti.tw - 1));
-            tj0 = (int32_t)fmax(cj, 0.0); tj1 = (int32_t)fmin(fj, (double)(ti.th - 1));
+          if (!empty) {   // clipped to the tile by selects (values in range here)
+            ti0 = ci > 0.0 ? (int32_t)ci : 0;
+            tj0 = cj > 0.0 ? (int32_t)cj : 0;
+            ti1 = fi < twm1 ? (int32_t)fi : ti.tw - 1;
+            tj1 = fj < thm1 ? (int32_t)fj : ti.th - 1;
           }
           int64_t cnt = (int64_t)(ti1 - ti0 + 1) * (tj1 - tj0 + 1);
           bool walk = !empty;
@@ -1171,7 +1192,7 @@ rectify_claim_kernel(RectArgs a) {
         }
       }
       t0 = b0;
-      t1 = b1;
+      et = eb;
     }
   }
 }
