@@ -533,6 +533,10 @@ struct RectArgs {
   float margin_scale;          // form margin factor (tests: >1 widens the exact-test band)
   int narrow;                  // dst_h * dst_w < 2^30, dst_w < 2^24: claims use 32-bit byte
                                // offsets and 24-bit multiplies
+  int key_shift;               // > 0: raster key = (qj << key_shift) | qi (lexicographic
+                               // order = raster order; decoded by a shift and a mask);
+                               // 0: qj * w + qi (decoded by a division)
+  uint32_t key_mul;            // 1 << key_shift, or w
   int tri_bit;                 // h * w < 2^31: a claim key is (raster key << 1) | (the
                                // reference's triangle is B), so K5b evaluates one triangle
   uint32_t* keys;              // (dst_h, dst_w) claim keys, 0xFFFFFFFF = free
@@ -1114,7 +1118,7 @@ rectify_claim_kernel(RectArgs a) {
           slow = true;
         }
       }
-      const uint32_t key = (uint32_t)qj * (uint32_t)a.w + (uint32_t)qi;
+      const uint32_t key = (uint32_t)qj * a.key_mul + (uint32_t)qi;   // raster order
       // claim keys of the two triangles (tri_bit: the low bit names B)
       const uint32_t key_a = claim_key(a, key, 1), key_b = claim_key(a, key, 2);
       // claims: the window pixels hit (row k / nw, column k % nw: exact in float
@@ -1410,11 +1414,17 @@ rectify_resolve_kernel(RectArgs a, FusedVar fv) {
             tri_b[r] = (key[r] & 1u) != 0;
             key[r] >>= 1;
           }
-          // key / w through the reciprocal, corrected to the exact quotient
-          // (key < 2^32: a 32-bit conversion, not the long int64 sequence)
-          int64_t j = (int64_t)(uint32_t)((double)key[r] * inv_w);
-          int64_t i = (int64_t)key[r] - j * a.w;
-          if (i < 0) { --j; i += a.w; } else if (i >= a.w) { ++j; i -= a.w; }
+          int64_t j, i;
+          if (a.key_shift > 0) {   // (qj << key_shift) | qi (uniform branch)
+            j = key[r] >> a.key_shift;
+            i = key[r] & (a.key_mul - 1u);
+          } else {
+            // key / w through the reciprocal, corrected to the exact quotient
+            // (key < 2^32: a 32-bit conversion, not the long int64 sequence)
+            j = (int64_t)(uint32_t)((double)key[r] * inv_w);
+            i = (int64_t)key[r] - j * a.w;
+            if (i < 0) { --j; i += a.w; } else if (i >= a.w) { ++j; i -= a.w; }
+          }
           // a key that is no quad's (inconsistent inputs) is reported and
           // dropped; selects, not a branch: the corner loads of all rows stay
           // in flight together
@@ -1671,6 +1681,16 @@ int rectify_ij_impl(const char* what, const double* x, const double* y, int64_t 
   // plain-key path of very large swaths on any input
   a.tri_bit = h * w < ((int64_t)1 << 31) &&
               xrs_testing_value(XRS_TESTING_RECTIFY_PLAIN_KEYS) == 0 ? 1 : 0;
+  // shifted raster keys when (h << b) fits the key (2^b >= w; the same order
+  // as qj * w + qi); the plain-key test knob keeps the division decode too
+  {
+    int b = 1;
+    while (((int64_t)1 << b) < w) ++b;
+    const int64_t limit = a.tri_bit ? ((int64_t)1 << 31) : (int64_t)UINT32_MAX;
+    a.key_shift = (h << b) <= limit && xrs_testing_value(XRS_TESTING_RECTIFY_PLAIN_KEYS) == 0
+                      ? b : 0;
+    a.key_mul = a.key_shift > 0 ? (uint32_t)1 << b : (uint32_t)w;
+  }
   if (!keys_ready)   // else filled by K4 (xrs_ij_bboxes_fill) or the caller
     XRS_HIP_CHECK(hipMemsetAsync(keys, 0xFF, (size_t)(dst_h * dst_w) * sizeof(uint32_t), st));
   {
