@@ -1,0 +1,56 @@
+"""K1 (config 5 bench workload) timed after a padding allocation of --pad-mb
+MB, so the source and target rasters land at other device addresses; run per
+library (XRS_LIBRARY) to see whether a work deal's rate depends on where the
+rasters sit (the channel hash) rather than on the deal alone.
+    XRS_LIBRARY=... python scripts/k1_pad_ab.py --pad-mb 0 [--steps 30]"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--pad-mb", type=int, default=0)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--tag", default="")
+    args = ap.parse_args()
+    import bench
+    import torch
+
+    from xcube_resampling_amd import kernels
+
+    dev = torch.device("cuda", 0)
+    pad = torch.empty(max(args.pad_mb, 1) << 20, dtype=torch.uint8, device=dev)
+    _, _, plan, _, _ = bench.workload(40960, 2048)
+    src = bench.synthetic_rows(0, plan.src_height, 40960, dev)
+    flags = kernels.ErrorFlags(dev)
+    out = torch.empty((1, 40960, 40960), device=dev, dtype=torch.float32)
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        kernels.reproject(src, plan, "bilinear", float("nan"), out_dtype=np.float32, out=out,
+                          flags=flags, check=False)
+
+    for _ in range(15):
+        step()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(args.steps):
+        step()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    print(json.dumps({"tag": args.tag, "pad_mb": args.pad_mb, "src_ptr": hex(src.data_ptr()),
+                      "out_ptr": hex(out.data_ptr()), "ms_per_launch": round(e0.elapsed_time(e1) / args.steps, 4)}))
+    del pad
+
+
+if __name__ == "__main__":
+    main()
