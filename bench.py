@@ -10,8 +10,8 @@ torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1
 --master-port <free> bench.py <same arguments>` as a child and exits with its
 status (launch_ranks); it refuses N above the visible GPU count.
 
-One "step" = one pass of the hot path (xrs_reproject: K1a axis tables + K1b
-gather) over the rank's share of ONE synthetic 40960^2 raster resident in
+One "step" = one pass of the hot path (xrs_reproject: the K1 gather, one
+launch; its work items resolve their own axis entries) over the rank's share of ONE synthetic 40960^2 raster resident in
 HBM.  Multi-GPU (configs[4]: one raster sharded over the GPUs):
 the target rows are split at row granularity (``sharding.band_shard``), each
 rank holds only the source rows its band reads and writes its own target
@@ -297,24 +297,71 @@ def shader_clock_ghz(lib, stream, blocks: int = 1024, spin: int = 3000) -> float
     return clock_probe_read(buf)
 
 
+KFD_NODES = "/sys/class/kfd/kfd/topology/nodes"
+
+
+def visible_gpu_count(nodes_dir: str = KFD_NODES, env=None) -> int:
+    """GPUs this process may use, counted WITHOUT touching HIP: the KFD
+    topology nodes with SIMDs (CPU nodes report simd_count 0), narrowed by
+    ROCR_VISIBLE_DEVICES / HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES as the
+    runtime narrows them.  torch.cuda.device_count() is not used: on ROCm it
+    falls back to hipGetDeviceCount when amdsmi does not answer, which starts
+    the HIP runtime in this parent.  Raises OSError when the topology cannot
+    be read (the launcher then refuses instead of guessing)."""
+    env = os.environ if env is None else env
+    gpus = 0
+    for name in sorted(os.listdir(nodes_dir)):
+        props = os.path.join(nodes_dir, name, "properties")
+        if not os.path.isfile(props):
+            continue
+        with open(props) as f:
+            for line in f:
+                key, _, val = line.partition(" ")
+                if key == "simd_count" and int(val) > 0:
+                    gpus += 1
+                    break
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        sel = env.get(var)
+        if sel is None:
+            continue
+        ids = [t for t in sel.split(",") if t.strip() != ""]
+        # the runtime stops at the first invalid ordinal ("-1" hides every GPU)
+        valid = 0
+        for t in ids:
+            t = t.strip()
+            if t.lstrip("-").isdigit() and 0 <= int(t) < gpus:
+                valid += 1
+            elif not t.lstrip("-").isdigit():      # a UUID: counted as one device
+                valid += 1
+            else:
+                break
+        gpus = valid
+    return gpus
+
+
 def launch_ranks(n: int, argv: list[str]) -> int:
     """`--gpus N` (N > 1) from a plain `python bench.py` call: start the N
     ranks, one process per GPU, under torch.distributed.run as a CHILD of this
-    parent, which has made no GPU call (never an exec after HIP init), and
-    return the child's exit status.  Rank 0 prints the JSON line; stdout and
-    stderr pass through.  With the nccl (RCCL) backend N must not exceed the
-    visible GPUs (torch.cuda.device_count() does not initialise HIP here)."""
+    parent, and return the child's exit status.  Rank 0 prints the JSON line;
+    stdout and stderr pass through.  The parent makes no HIP call (never an
+    exec after HIP init, and no runtime state to inherit): with the nccl
+    (RCCL) backend it counts the visible GPUs from the KFD topology
+    (visible_gpu_count) and refuses, status 2, when there are fewer than N or
+    the topology cannot be read."""
     import socket
 
     backend = os.environ.get("XRS_BENCH_BACKEND", "nccl")
     cmd_tail = [os.path.abspath(__file__), *argv]
     if backend == "nccl" and "--dry-run" not in argv:
-        import torch
-
-        have = torch.cuda.device_count()
+        try:
+            have = visible_gpu_count()
+        except OSError as e:
+            have, why = 0, f" (KFD topology unreadable: {e})"
+        else:
+            why = ""
         if have < n:
-            print(f"bench: --gpus {n} needs {n} visible GPUs, found {have}; on an {n}-GPU node "
-                  f"run: python -m torch.distributed.run --nnodes=1 --nproc-per-node {n} "
+            print(f"bench: --gpus {n} needs {n} visible GPUs, found {have}{why}; on an {n}-GPU "
+                  f"node run: python -m torch.distributed.run --nnodes=1 --nproc-per-node {n} "
                   f"--master-addr 127.0.0.1 --master-port 29500 bench.py {' '.join(argv)}",
                   file=sys.stderr)
             return 2
@@ -574,7 +621,7 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / peak, 4),
                 "traffic": traffic["hbm_bytes_per_launch"] if traffic else None,
-                "kernel": "gather_separable_kernel<float,float,1> (+ axis_tables_kernel<1>, <1%)",
+                "kernel": "gather_separable_kernel<float,float,1>",
                 "kernel_ms": round(max_kernel_ms, 4),
                 "algorithmic_bytes": int(alg_bytes),
                 "copy_GBs": round(copy_all, 1),

@@ -116,8 +116,9 @@ int xrs_copy_async(void* dst, const void* src, int64_t bytes, void* stream);
  *      ntiles = ceil(dst_h/tile_h) * ceil(dst_w/tile_w), row-major.
  * dst_dtype: = src_dtype for nearest/triangular; float32 or float64 for
  *      bilinear (the reference yields float64 there; float32 = declared dtype).
- * workspace: device scratch of xrs_reproject_workspace_size(...) bytes (the
- *      per-(tile, column) / (tile, row) index tables of coord_mode 0).
+ * workspace: device scratch of xrs_reproject_workspace_size(...) bytes; 0
+ *      since round 5 (K1's work items resolve their own axis entries), so
+ *      NULL / 0 may be passed.
  * A source row may span at most 2 GiB (src_w * element size), else XRS_ERR_ARG.
  * ------------------------------------------------------------------------- */
 int64_t xrs_reproject_workspace_size(int64_t dst_h, int64_t dst_w, int64_t tile_h,
@@ -342,8 +343,8 @@ int xrs_rectify_var(const double* ij, int64_t ij_sn, int64_t dst_h, int64_t dst_
  *                                         pixel floor by the exact division
  *   XRS_TESTING_RECTIFY_MARGIN            k > 1: K5 widens its float32 form margin
  *                                         k-fold (more pixels take the exact test)
- *   XRS_TESTING_REPROJECT_XCD_GROUP       k > 0: K1b deals column groups of k
- *                                         segments instead of whole bands (0)
+ *   (6: retired in round 5 — K1's column-group deal, measured slower, left
+ *    the product; setting it is accepted and changes nothing)
  *   XRS_TESTING_RECTIFY_PLAIN_KEYS        1: K5 claims with plain raster keys and
  *                                         the resolve tests both triangles (the
  *                                         path of swaths of 2^31 points or more)
@@ -354,7 +355,6 @@ int xrs_rectify_var(const double* ij, int64_t ij_sn, int64_t dst_h, int64_t dst_
 #define XRS_TESTING_AFFINE_GENERIC 3
 #define XRS_TESTING_RECTIFY_EXACT 4
 #define XRS_TESTING_RECTIFY_MARGIN 5
-#define XRS_TESTING_REPROJECT_XCD_GROUP 6
 #define XRS_TESTING_RECTIFY_PLAIN_KEYS 7
 #define XRS_TESTING_NUM_KNOBS 8
 int64_t xrs_testing_set(int knob, int64_t value);

@@ -7,6 +7,7 @@ import csv
 import os
 
 import numpy as np
+import pytest
 
 
 def test_source_pixels_read_matches_band_sum():
@@ -141,3 +142,47 @@ def test_gpus_flag_refuses_more_ranks_than_gpus():
     r, line = _run_bench(["--gpus", "4", "--steps", "1", "--warmup", "0"], timeout=120)
     assert r.returncode == 2 and line is None
     assert "--nproc-per-node 4" in r.stderr and "--master-addr 127.0.0.1" in r.stderr
+
+
+def _fake_kfd(tmp_path, simds):
+    nodes = tmp_path / "nodes"
+    for i, n in enumerate(simds):
+        d = nodes / str(i)
+        d.mkdir(parents=True)
+        (d / "properties").write_text(f"cpu_cores_count 0\nsimd_count {n}\nmax_waves_per_simd 8\n")
+    return str(nodes)
+
+
+def test_visible_gpu_count_reads_kfd_topology_and_visibility(tmp_path):
+    """The launcher's GPU count comes from the KFD topology (nodes with
+    SIMDs; the CPU node has none), narrowed by the *_VISIBLE_DEVICES lists as
+    the runtime narrows them."""
+    import bench
+
+    nodes = _fake_kfd(tmp_path, [0] + [1024] * 8)     # one CPU node + 8 GPUs
+    assert bench.visible_gpu_count(nodes, env={}) == 8
+    assert bench.visible_gpu_count(nodes, env={"HIP_VISIBLE_DEVICES": "0,3"}) == 2
+    assert bench.visible_gpu_count(nodes, env={"ROCR_VISIBLE_DEVICES": "1,2,3",
+                                               "HIP_VISIBLE_DEVICES": "0"}) == 1
+    assert bench.visible_gpu_count(nodes, env={"CUDA_VISIBLE_DEVICES": "-1"}) == 0
+    assert bench.visible_gpu_count(nodes, env={"HIP_VISIBLE_DEVICES": "0,9,1"}) == 1
+    assert bench.visible_gpu_count(nodes, env={"HIP_VISIBLE_DEVICES": ""}) == 0
+    with pytest.raises(OSError):
+        bench.visible_gpu_count(str(tmp_path / "missing"), env={})
+
+
+def test_launcher_count_does_not_initialise_hip():
+    """Counting GPUs for `--gpus N` leaves torch's HIP runtime untouched in
+    the parent (torch.cuda.device_count() may fall back to
+    hipGetDeviceCount)."""
+    import subprocess
+    import sys
+
+    from conftest import ROOT
+
+    code = ("import sys, torch; sys.path.insert(0, %r); import bench\n"
+            "try:\n    bench.visible_gpu_count()\nexcept OSError:\n    pass\n"
+            "assert not torch.cuda.is_initialized()\nprint('ok')\n" % ROOT)
+    r = subprocess.run([sys.executable, "-c", code], stdout=subprocess.PIPE,
+                       stderr=subprocess.PIPE, text=True, timeout=120)
+    assert r.returncode == 0 and r.stdout.strip() == "ok", r.stderr[-2000:]

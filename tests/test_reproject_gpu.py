@@ -38,16 +38,16 @@ def test_kernel_matches_reference_bitwise(case, interp):
     assert_bitwise_equal(out.cpu().numpy(), g[f"out_{interp}"], f"{case}/{interp}")
 
 
-@pytest.mark.parametrize("band,bpc,group", [(5, 0, 0), (1, 0, 0), (32, 1, 0), (7, 1, 0),
-                                            (8, 0, 4), (3, 1, 2), (4, 0, 1), (2, 0, 3),
-                                            (1, 1, 5)])
-def test_work_shapes_are_bit_identical(band, bpc, group):
-    """K1's work decomposition (target rows per work item, grid cap, K1b's
-    column-group deal instead of whole bands) changes only which block
-    computes a pixel: items that split tiles (5 / 1 rows), a single block per
-    CU (grid-stride loop), column groups of 1-5 segments (a narrower last
-    group) — all reproduce the reference bit for bit.  The shapes are forced through the test-only knobs
-    (xrs_testing_set); the product never reads them from the environment."""
+@pytest.mark.parametrize("band,bpc", [(5, 0), (1, 0), (32, 1), (7, 1), (8, 0), (3, 1), (4, 0),
+                                      (2, 0), (1, 1), (64, 0), (65, 0), (100, 1), (200, 0)])
+def test_work_shapes_are_bit_identical(band, bpc):
+    """K1's work decomposition (target rows per work item, grid cap) changes
+    only which block computes a pixel: items that split tiles (5 / 1 rows), a
+    single block per CU (grid-stride loop), items taller than the 64 rows one
+    resolve of the row entries covers (65-200 rows: the entries are resolved
+    again every 64 rows) — all reproduce the reference bit for bit.  The
+    shapes are forced through the test-only knobs (xrs_testing_set); the
+    product never reads them from the environment."""
     import torch
 
     import xcube_resampling_amd as xrs
@@ -63,11 +63,10 @@ def test_work_shapes_are_bit_identical(band, bpc, group):
         src = torch.from_numpy(g["data"]).cuda()
         for interp in ("nearest", "bilinear", "triangular"):
             with testing_knob("reproject_band", band), \
-                    testing_knob("reproject_blocks_per_cu", bpc), \
-                    testing_knob("reproject_xcd_group", group):
+                    testing_knob("reproject_blocks_per_cu", bpc):
                 out = kernels.reproject(src, plan, interp, g["fill"].item())
             assert_bitwise_equal(out.cpu().numpy(), g[f"out_{interp}"],
-                                 f"{case}/{interp} band={band} bpc={bpc} group={group}")
+                                 f"{case}/{interp} band={band} bpc={bpc}")
 
 
 @pytest.mark.parametrize("case", NO_DOWNSCALE)

@@ -168,8 +168,8 @@ PROJ_KINDS = {"webmerc_fwd": 1, "webmerc_inv": 2, "tmerc_fwd": 3, "tmerc_inv": 4
 MAX_PROJ_STEPS = 4
 
 TESTING_KNOBS = {"reproject_band": 1, "reproject_blocks_per_cu": 2, "affine_generic": 3,
-                 "rectify_exact": 4, "rectify_margin": 5, "reproject_xcd_group": 6,
-                 "rectify_plain_keys": 7}
+                 "rectify_exact": 4, "rectify_margin": 5,
+                 "rectify_plain_keys": 7}   # 6: retired (K1's column-group deal, round 5)
 
 
 class testing_knob:

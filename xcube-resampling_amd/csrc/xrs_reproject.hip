@@ -7,24 +7,23 @@
 // reproject.py:385-469) is computed by the host and passed as small tables.
 //
 // Separable CRS pairs (coord_mode 0: target x -> source x only, y -> y only,
-// e.g. EPSG:3857 -> EPSG:4326) run in two launches:
-//   K1a axis_tables : for every (tile, column) and (tile, row) resolve the
-//                     reference's per-pixel index math ONCE — ix = (sx-x0)/res,
-//                     floor/ceil/rint, int16 cast, python-style window wrap,
-//                     window -> source index, pad -> "outside" — into
-//                     {idx_floor, idx_ceil, frac} entries (16 B).  Bit-exact
-//                     because for separable transforms the per-pixel ix only
-//                     depends on the column (iy on the row).
-//   K1b gather      : the HBM-bound part.  One work item = one tile x one
-//                     512-column segment x one band of kBand rows, so the tile
-//                     (and every row entry) is block-uniform: row pointers are
-//                     scalar, lane offsets 32-bit.  Lanes take consecutive
-//                     columns (each wave-load touches ~256 contiguous source
-//                     bytes); the loads of kRows target rows are issued before
-//                     any is consumed (memory-level parallelism); stores are
-//                     non-temporal.  The ceil/floor overlap between neighbouring
-//                     rows and columns is served by L1/L2 (PMC: HBM traffic =
-//                     the algorithmic bytes).
+// e.g. EPSG:3857 -> EPSG:4326) run ONE launch, K1b, the HBM-bound gather.
+// One work item = one tile x one 512-column segment x one band of kBand rows,
+// so the tile (and every row entry) is block-uniform: row pointers are scalar,
+// lane offsets 32-bit.  The item resolves the reference's per-pixel index math
+// itself — ix = (sx-x0)/res, floor/ceil/rint, int16 cast, python-style window
+// wrap, window -> source index, pad -> "outside" — for its own columns (one
+// per lane and column, from the source-CRS column coordinate src_x[c]) and its
+// own rows (lane q of every wave resolves row r0 + q; the batch reads the
+// entries back by readlane).  Bit-exact because for separable transforms the
+// per-pixel ix only depends on the column (iy on the row).  Lanes take
+// consecutive columns (each wave-load touches ~256 contiguous source bytes);
+// the loads of kRows target rows are issued before any is consumed
+// (memory-level parallelism); stores are non-temporal.  The ceil/floor overlap
+// between neighbouring rows and columns is served by L1/L2.
+// (Rounds 1-4 resolved the entries in a separate K1a launch into 16-byte
+// tables; every item re-fetched its 512 x entries through the fabric: reads
+// 1.154x the algorithmic bytes.  DESIGN.md §3 "K1, round 5".)
 // Non-separable pairs (coord_mode 1: 2-D coordinate tables) run K1c, the same
 // work decomposition with the index math done per pixel.
 //
@@ -65,7 +64,6 @@ struct K1Shape {
   static constexpr int segw = kThreads * px;
 };
 constexpr int kRows2D = 2;                   // K1c: target rows per step (2-D tables; 4: slower)
-constexpr int kColGroup = 0;                 // K1b deal: 0 = band by band (see colgroup_item)
 
 struct AxisEntry {   // one resolved column (or row) of one tile
   int32_t f;         // source index of floor(ix) (nearest: of rint(ix)); -1 = outside source
@@ -89,8 +87,6 @@ struct Geometry {
   int64_t band;   // target rows per work item of the gathers
   int64_t segw;   // target columns per work item (kThreads x columns per thread)
   int64_t band_first;   // bands of tile row ty0 above row_begin (not in the work list)
-  int64_t colgroup;     // K1b: 0 = bands dealt to the XCDs in turn (product); k > 0 =
-                        // column groups of k segments (colgroup_item; test knob)
 };
 
 // numpy fancy index on a window axis of length `win` with an int16 index:
@@ -149,44 +145,6 @@ __device__ inline AxisEntry resolve_axis(double coord, float origin, double res,
   return e;
 }
 
-// ---- K1a: axis tables ------------------------------------------------------
-template <int INTERP>
-__global__ void __launch_bounds__(kThreads)
-axis_tables_kernel(Geometry g, int64_t ty0, int64_t ty1, AxisEntry* __restrict__ xtab,
-                   AxisEntry* __restrict__ ytab) {
-  // only the tile rows [ty0, ty1) holding [row_begin, row_end) are resolved:
-  // the gathers read no other entries (a rank's row band pays for its band)
-  const int64_t t0 = ty0 * g.ntiles_x, ntiles = (ty1 - ty0) * g.ntiles_x;
-  const int64_t nx = ntiles * g.tile_w, total = nx + ntiles * g.tile_h;
-  xtab += t0 * g.tile_w;
-  ytab += t0 * g.tile_h;
-  int32_t eflags = 0;
-  for (int64_t idx = (int64_t)blockIdx.x * kThreads + threadIdx.x; idx < total;
-       idx += (int64_t)gridDim.x * kThreads) {
-    if (idx < nx) {
-      const int64_t tl = idx / g.tile_w, k = idx - tl * g.tile_w, t = t0 + tl;
-      const int64_t c = (t % g.ntiles_x) * g.tile_w + k;
-      const int64_t r0 = (t / g.ntiles_x) * g.tile_h;
-      AxisEntry e{-1, -1, 0.0};
-      // tiles outside the computed rows [row_begin, row_end) are never read
-      if (c < g.dst_w && r0 < g.row_end && r0 + g.tile_h > g.row_begin)
-        e = resolve_axis<INTERP>(g.src_x[c], g.tile_x0[t], g.x_res, g.win_w, g.tile_win[2 * t],
-                                 g.src_w, 0, g.src_w, eflags);
-      xtab[idx] = e;
-    } else {
-      const int64_t j = idx - nx;
-      const int64_t tl = j / g.tile_h, k = j - tl * g.tile_h, t = t0 + tl;
-      const int64_t r = (t / g.ntiles_x) * g.tile_h + k;
-      AxisEntry e{-1, -1, 0.0};
-      if (r >= g.row_begin && r < g.row_end)
-        e = resolve_axis<INTERP>(g.src_y[r], g.tile_y0[t], g.neg_y_res, g.win_h,
-                                 g.tile_win[2 * t + 1], g.src_h, g.src_row0, g.src_rows, eflags);
-      ytab[j] = e;
-    }
-  }
-  if (eflags) atomicOr(g.err_flags, eflags);
-}
-
 // ---- interpolation of one pixel (reproject.py:304-314, 326-328) ------------
 template <typename T, int INTERP>
 __device__ inline double interp4(T v00, T v01, T v10, T v11, double dx, double dy) {
@@ -228,14 +186,11 @@ struct GatherArgs {
   void* dst;
   int64_t dst_sn, dst_sy;
   double fill;
-  const AxisEntry* xtab;
-  const AxisEntry* ytab;
 };
 
 // Work decomposition shared by K1b/K1c: bands of kBand rows inside one tile row
-// x segments of kSegW columns inside one tile column, band-major; K1c's XCDs
-// take whole bands in turn (xcd_groups, group = nsegs), K1b's walk column
-// groups (colgroup_item).  The list starts at
+// x segments of kSegW columns inside one tile column, band-major; the XCDs
+// take whole bands in turn (XCD x: bands x, x + 8, ...).  The list starts at
 // the band holding row_begin and ends at the band holding row_end - 1, so a
 // row band of the raster (a rank's share) has no empty items (blocks are dealt
 // to XCDs round-robin whatever their cost: empty items would idle an XCD).
@@ -261,73 +216,49 @@ __device__ inline bool work_item(const Geometry& g, int64_t w, int64_t ty0, int6
   return it.r0 < it.r1 && it.c0 < it.c1;
 }
 
-// K1b's deal.  Every item reads its segment's 512 x-table entries (16 B
-// each: 8 KB beside 64 KB of source taps).  Dealt band by band (the
-// product), an XCD meets the same segment again only one band later — about
-// 10 MB of streamed taps and stores through its 4 MB L2 — so every item
-// fetches its entries through the fabric again: an identity launch reads
-// 1.125x its bytes at the L2's memory side, the bench launch 1.154x
-// (size-resolved request counters, profiles/r04_k1_colgroup_ab.jsonl).  The
-// column-group deal below orders the items by (group of G adjacent
-// segments, band, segment in the group) and gives each XCD one contiguous
-// eighth: an XCD walks down G segment columns, so x-table slices, band seams
-// and segment seams come from its L2 (identity 1.004x, bench 1.043x) — and
-// K1 runs 2-15 % SLOWER (G = 1 / 2 / 4 / 8: 2.86-2.92 / 2.63-2.64 /
-// 2.59-2.79 / 2.51-2.53 ms against 2.46-2.49 ms band by band, interleaved on
-// one box).  The re-fetched slices are Infinity-Cache hits; what costs is
-// the DRAM pattern: band by band, the requests in flight sweep whole rows,
-// while narrow column groups scatter them over many rows (plain copies show
-// the same: the wider the address window in flight, the slower, 6.2 TB/s at
-// 4 KB per block down to 5.2 TB/s at 64 KB, scripts/xcd_probe.py).  Kept as
-// the XRS_TESTING_REPROJECT_XCD_GROUP alternative (bit-identical results).
-// Returns the band-major index work_item() decodes, or -1 past the list.
-__device__ inline int64_t colgroup_item(int64_t nwork, int64_t nsegs, int64_t G, int64_t idx) {
-  if (idx >= nwork) return -1;
-  const int64_t nbands = nwork / nsegs;
-  const int64_t gsize = nbands * G;          // items of a full group
-  const int64_t gi = idx / gsize;
-  const int64_t r = idx - gi * gsize;
-  const int64_t s0 = gi * G;
-  const int64_t gw = min(G, nsegs - s0);     // the last group may be narrower
-  const int64_t band = r / gw;
-  return band * nsegs + s0 + (r - band * gw);
-}
-
 // ---- K1b: separable gather --------------------------------------------------
 // No rows are carried between target rows: every target row loads its two
 // source rows (their overlap with the neighbouring rows is served by L1/L2),
 // but the loads of kRows target rows are independent and in flight together.
+// The item's axis entries are resolved in the item (header): its columns'
+// from src_x (8 B per column, L2-resident: the whole raster's column
+// coordinates are 320 KB), its rows' by lane, 64 rows per resolve.
 template <typename T, typename O, int INTERP>
 __global__ void __launch_bounds__(kThreads)
 gather_separable_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t bands_per_tile,
                         int64_t segs_per_tile, int64_t nwork) {
   const Geometry& g = a.g;
   constexpr int kPx = K1Shape<O>::px, kRows = K1Shape<O>::rows;
+  static_assert(64 % kRows == 0, "a 64-row entry chunk holds whole batches");
   const T fill = Conv<T>::from_f64(a.fill);
-  // the XCDs take whole bands in turn (XCD x: bands x, x + 8, ...); the
-  // column-group deal (colgroup_item) is the test knob's alternative
-  const int64_t xcd = blockIdx.x & 7, per = (nwork + 7) / 8;
+  const int lane = (int)(threadIdx.x & 63);
+  int32_t eflags = 0;
+  // the XCDs take whole bands in turn (XCD x: bands x, x + 8, ...)
+  const int64_t xcd = blockIdx.x & 7;
   for (int64_t i = blockIdx.x >> 3;; i += gridDim.x >> 3) {
-    int64_t w;
-    if (g.colgroup > 0) {
-      w = i < per ? colgroup_item(nwork, nsegs, g.colgroup, xcd * per + i) : -1;
-      if (w < 0) break;
-    } else {
-      const int64_t m = i / nsegs;
-      w = (m * 8 + xcd) * nsegs + (i - m * nsegs);
-      if (w >= nwork) break;
-    }
+    const int64_t m = i / nsegs;
+    const int64_t w = (m * 8 + xcd) * nsegs + (i - m * nsegs);
+    if (w >= nwork) break;
     WorkItem it;
     if (!work_item(g, w, ty0, nsegs, bands_per_tile, segs_per_tile, it)) continue;
-    const AxisEntry* xt = a.xtab + it.t * g.tile_w + (it.c0 - it.tx * g.tile_w);
     const int ncols = (int)(it.c1 - it.c0);
+    // this item's columns: coordinates requested together, then resolved
+    const float x0 = g.tile_x0[it.t];
+    const int64_t wi0 = g.tile_win[2 * it.t];
+    double sx[kPx];
+#pragma unroll
+    for (int k = 0; k < kPx; ++k) {
+      const int lc = (int)threadIdx.x + k * kThreads;
+      sx[k] = g.src_x[it.c0 + min(lc, ncols - 1)];
+    }
     int32_t cf[kPx], cc[kPx];
     double dx[kPx];
 #pragma unroll
     for (int k = 0; k < kPx; ++k) {
       const int lc = (int)threadIdx.x + k * kThreads;
       AxisEntry e{-1, -1, 0.0};
-      if (lc < ncols) e = xt[lc];
+      if (lc < ncols)
+        e = resolve_axis<INTERP>(sx[k], x0, g.x_res, g.win_w, wi0, g.src_w, 0, g.src_w, eflags);
       cf[k] = e.f;
       cc[k] = e.c;
       dx[k] = e.d;
@@ -340,7 +271,13 @@ gather_separable_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t bands_
       fo[k] = (uint32_t)max(cf[k], 0) * (uint32_t)sizeof(T);
       co[k] = (uint32_t)max(cc[k], 0) * (uint32_t)sizeof(T);
     }
-    const AxisEntry* yt = a.ytab + it.t * g.tile_h - it.ty * g.tile_h;
+    // this item's rows: lane q holds the entry of row ybase + q (rows past
+    // r1 hold "outside", as the batches expect); one resolve per 64 rows
+    const float y0 = g.tile_y0[it.t];
+    const int64_t wj0 = g.tile_win[2 * it.t + 1];
+    int32_t yf = -1, yc = -1;
+    double yd = 0.0;
+    int64_t ybase = it.r0 - 64;
     for (int64_t sn = 0; sn < a.n; ++sn) {
       const T* __restrict__ src = static_cast<const T*>(a.src) + sn * a.src_sn;
       O* __restrict__ dst = static_cast<O*>(a.dst) + sn * a.dst_sn - g.row_begin * a.dst_sy + it.c0;
@@ -361,6 +298,18 @@ gather_separable_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t bands_
         }
       };
       for (int64_t r = it.r0; r < it.r1; r += kRows) {
+        if (r < ybase || r >= ybase + 64) {   // wave-uniform; once per item for bands <= 64
+          ybase = r;
+          const int64_t ry = r + lane;
+          AxisEntry e{-1, -1, 0.0};
+          if (ry < it.r1)
+            e = resolve_axis<INTERP>(g.src_y[ry], y0, g.neg_y_res, g.win_h, wj0, g.src_h,
+                                     g.src_row0, g.src_rows, eflags);
+          yf = e.f;
+          yc = e.c;
+          yd = e.d;
+        }
+        const int j0 = (int)(r - ybase);
         AxisEntry ye[kRows];
         T v[kRows][4][kPx];
         // all taps of kRows target rows requested before any is used; entries
@@ -368,7 +317,12 @@ gather_separable_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t bands_
         // and are replaced by the fill value below
 #pragma unroll
         for (int q = 0; q < kRows; ++q) {
-          ye[q] = (r + q < it.r1) ? yt[r + q] : AxisEntry{-1, -1, 0.0};
+          ye[q].f = __builtin_amdgcn_readlane(yf, j0 + q);
+          ye[q].c = __builtin_amdgcn_readlane(yc, j0 + q);
+          const uint64_t db = __builtin_bit_cast(uint64_t, yd);
+          const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)db, j0 + q);
+          const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(db >> 32), j0 + q);
+          ye[q].d = __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
           const __amdgpu_buffer_rsrc_t rf =
               row_rsrc(src + (int64_t)max(ye[q].f, 0) * a.src_sy, row_bytes);
           const __amdgpu_buffer_rsrc_t rc =
@@ -406,6 +360,7 @@ gather_separable_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t bands_
       if (rprev >= 0) flush(rprev);
     }
   }
+  if (eflags) atomicOr(g.err_flags, eflags);
 }
 
 // ---- one target pixel of every dim-0 slice, from its resolved entries -------
@@ -656,8 +611,6 @@ inline Work work_of(const GatherArgs& a, int64_t band = kBand, int64_t segw = kS
   // them so the tests cover items that split tiles and the grid-stride loop
   const int64_t band_knob = xrs_testing_value(XRS_TESTING_REPROJECT_BAND);
   k.args.g.band = band_knob > 0 ? band_knob : band;
-  const int64_t group_knob = xrs_testing_value(XRS_TESTING_REPROJECT_XCD_GROUP);
-  k.args.g.colgroup = group_knob > 0 ? group_knob : kColGroup;
   k.args.g.segw = segw;
   k.bands_per_tile = (g.tile_h + k.args.g.band - 1) / k.args.g.band;
   k.segs_per_tile = (g.tile_w + k.args.g.segw - 1) / k.args.g.segw;
@@ -675,18 +628,9 @@ inline Work work_of(const GatherArgs& a, int64_t band = kBand, int64_t segw = kS
 }
 
 template <typename T, typename O, int INTERP>
-int launch(const GatherArgs& a, int coord_mode, AxisEntry* xtab, AxisEntry* ytab,
-           hipStream_t stream) {
-  const Geometry& g = a.g;
+int launch(const GatherArgs& a, int coord_mode, hipStream_t stream) {
   Work k = coord_mode == 0 ? work_of(a, K1Shape<O>::band, K1Shape<O>::segw) : work_of(a);
   if (coord_mode == 0) {
-    const int64_t ntab = g.ntiles_x * (k.ty1 - k.ty0) * (g.tile_w + g.tile_h);
-    const int nbt = grid_blocks(ntab, kThreads, 256 * 8);
-    hipLaunchKernelGGL((axis_tables_kernel<INTERP>), dim3(nbt), dim3(kThreads), 0, stream, g,
-                       k.ty0, k.ty1, xtab, ytab);
-    XRS_HIP_CHECK(hipGetLastError());
-    k.args.xtab = xtab;
-    k.args.ytab = ytab;
     hipLaunchKernelGGL((gather_separable_kernel<T, O, INTERP>), dim3(k.nb), dim3(kThreads), 0,
                        stream, k.args, k.ty0, k.nsegs, k.bands_per_tile, k.segs_per_tile, k.nwork);
   } else {
@@ -752,11 +696,12 @@ int launch_proj_second(int k1, const GatherArgs& a, const XrsProjStep& s0,
 }  // namespace
 }  // namespace xrs
 
+// K1 needs no scratch since round 5 (each work item resolves its own axis
+// entries); the entry point stays so a binding sized by it keeps working.
 extern "C" int64_t xrs_reproject_workspace_size(int64_t dst_h, int64_t dst_w, int64_t tile_h,
                                                 int64_t tile_w, int coord_mode) {
-  if (coord_mode != 0 || dst_h < 1 || dst_w < 1 || tile_h < 1 || tile_w < 1) return 0;
-  const int64_t ntiles = ((dst_h + tile_h - 1) / tile_h) * ((dst_w + tile_w - 1) / tile_w);
-  return ntiles * (tile_w + tile_h) * (int64_t)sizeof(xrs::AxisEntry);
+  (void)dst_h; (void)dst_w; (void)tile_h; (void)tile_w; (void)coord_mode;
+  return 0;
 }
 
 extern "C" int xrs_reproject(const void* src, int src_dtype, int64_t n, int64_t src_h,
@@ -814,23 +759,20 @@ extern "C" int xrs_reproject(const void* src, int src_dtype, int64_t n, int64_t 
   g.ntiles_y = (dst_h + tile_h - 1) / tile_h;
   g.src_x = src_x; g.src_y = src_y; g.tile_x0 = tile_x0; g.tile_y0 = tile_y0;
   g.tile_win = tile_win; g.win_h = win_h; g.win_w = win_w;
-  g.x_res = x_res; g.neg_y_res = -y_res; g.err_flags = err_flags; g.band = kBand; g.segw = kSegW; g.band_first = 0; g.colgroup = kColGroup;
+  g.x_res = x_res; g.neg_y_res = -y_res; g.err_flags = err_flags; g.band = kBand; g.segw = kSegW; g.band_first = 0;
   a.src = src; a.n = n; a.src_sn = src_sn; a.src_sy = src_sy;
   a.dst = dst; a.dst_sn = dst_sn; a.dst_sy = dst_sy; a.fill = fill;
-  a.xtab = a.ytab = nullptr;
-  AxisEntry* xtab = static_cast<AxisEntry*>(workspace);
-  AxisEntry* ytab = xtab ? xtab + g.ntiles_x * g.ntiles_y * tile_w : nullptr;
   hipStream_t st = static_cast<hipStream_t>(stream);
 
   return dispatch_dtype(src_dtype, [&](auto tag) -> int {
     using T = decltype(tag);
     if (interp == XRS_INTERP_NEAREST)
-      return launch<T, T, XRS_INTERP_NEAREST>(a, coord_mode, xtab, ytab, st);
+      return launch<T, T, XRS_INTERP_NEAREST>(a, coord_mode, st);
     if (interp == XRS_INTERP_TRIANGULAR)
-      return launch<T, T, XRS_INTERP_TRIANGULAR>(a, coord_mode, xtab, ytab, st);
+      return launch<T, T, XRS_INTERP_TRIANGULAR>(a, coord_mode, st);
     if (dst_dtype == XRS_DTYPE_F32)
-      return launch<T, float, XRS_INTERP_BILINEAR>(a, coord_mode, xtab, ytab, st);
-    return launch<T, double, XRS_INTERP_BILINEAR>(a, coord_mode, xtab, ytab, st);
+      return launch<T, float, XRS_INTERP_BILINEAR>(a, coord_mode, st);
+    return launch<T, double, XRS_INTERP_BILINEAR>(a, coord_mode, st);
   });
 }
 
@@ -897,10 +839,9 @@ extern "C" int xrs_reproject_proj(const void* src, int src_dtype, int64_t n, int
   g.ntiles_y = (dst_h + tile_h - 1) / tile_h;
   g.src_x = grid_x; g.src_y = grid_y; g.tile_x0 = tile_x0; g.tile_y0 = tile_y0;
   g.tile_win = tile_win; g.win_h = win_h; g.win_w = win_w;
-  g.x_res = x_res; g.neg_y_res = -y_res; g.err_flags = err_flags; g.band = kBand; g.segw = kSegW; g.band_first = 0; g.colgroup = kColGroup;
+  g.x_res = x_res; g.neg_y_res = -y_res; g.err_flags = err_flags; g.band = kBand; g.segw = kSegW; g.band_first = 0;
   a.src = src; a.n = n; a.src_sn = src_sn; a.src_sy = src_sy;
   a.dst = dst; a.dst_sn = dst_sn; a.dst_sy = dst_sy; a.fill = fill;
-  a.xtab = a.ytab = nullptr;
   XrsProjStep s0{}, s1{};
   if (nsteps > 0) s0 = steps[0];
   if (nsteps > 1) s1 = steps[1];
