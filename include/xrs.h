@@ -78,8 +78,12 @@ const char* xrs_last_error(void);
  * page boundary and `bytes` a multiple of the page size (else XRS_ERR_ARG —
  * a malloc'd numpy array shares its edge pages with its neighbours); returns
  * XRS_OK, 1 when the range was already registered (the caller must then NOT
- * unregister it), or XRS_ERR_HIP.  xrs_host_unregister drains the device
- * (every stream) before unpinning, so no queued copy outlives the pinning.
+ * unregister it), or XRS_ERR_HIP.  xrs_host_unregister drains every visible
+ * device (every stream) before unpinning, so no queued copy outlives the
+ * pinning; the calling thread's current device is restored.  It stalls work
+ * unrelated to the range, and must not run while another thread captures a
+ * graph: bindings that know which streams used the range may synchronise
+ * those instead and unregister outside capture windows.
  * ------------------------------------------------------------------------- */
 int xrs_host_register(void* ptr, int64_t bytes);
 int xrs_host_unregister(void* ptr);
@@ -98,6 +102,14 @@ int xrs_copy_async(void* dst, const void* src, int64_t bytes, void* stream);
  *   sx, sy = coordinate of the pixel centre in the source CRS
  *            coord_mode 0 (separable): sx = src_x[c], sy = src_y[r]
  *            coord_mode 1 (2-D):       sx = src_x[r*dst_w+c], sy = src_y[...]
+ *            coord_mode 2 (separable, column generators): sy = src_y[r];
+ *              src_x = ntiles_x records {start, stop, step, n} (f64 x 4) and
+ *              then (m1, m2); for c in tile column tx, k = c - tx*tile_w:
+ *              v = k == n-1 ? stop : k*step + start, sx = (v*m1)*m2 — dask's
+ *              blockwise linspace of the target pixel centres and the
+ *              separable transformation's scalings, evaluated with the
+ *              host's operation order.  The caller must have checked that
+ *              these values equal its src_x bit for bit (0 B/column read).
  *   ix = (sx - (double)tile_x0[t]) / x_res           (reproject.py:278)
  *   iy = (sy - (double)tile_y0[t]) / -y_res          (reproject.py:279)
  *   window index -> int16 as numpy, python-style negative wrap in

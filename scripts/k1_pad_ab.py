@@ -21,6 +21,9 @@ def main():
     ap.add_argument("--pad-mb", type=int, default=0)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--tag", default="")
+    ap.add_argument("--no-xgen", action="store_true",
+                    help="read the src_x table (coord_mode 0; libraries before round 5 "
+                         "know no coord_mode 2)")
     args = ap.parse_args()
     import bench
     import torch
@@ -30,6 +33,9 @@ def main():
     dev = torch.device("cuda", 0)
     pad = torch.empty(max(args.pad_mb, 1) << 20, dtype=torch.uint8, device=dev)
     _, _, plan, _, _ = bench.workload(40960, 2048)
+    if args.no_xgen:
+        import dataclasses
+        plan = dataclasses.replace(plan, x_gen=None, _device_cache={})
     src = bench.synthetic_rows(0, plan.src_height, 40960, dev)
     flags = kernels.ErrorFlags(dev)
     out = torch.empty((1, 40960, 40960), device=dev, dtype=torch.float32)

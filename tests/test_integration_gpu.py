@@ -75,3 +75,47 @@ def test_integration_stub_on_reference_window_outputs(case, interp):
                                 (ttile[1], ttile[0]), (tsize[1], tsize[0]), float(g["x_res"]),
                                 float(g["y_res"]), interp, g["fill"].item())
     assert_bitwise_equal(out, g[f"out_{interp}"], f"{case}/{interp}")
+
+
+def test_integration_stub_device_per_block_from_threads():
+    """The stub's device argument as a dask threaded scheduler would use it:
+    blocks (the dim-0 slices of two golden rasters, twice) run from
+    four threads, each on device_of_block(k) — every visible GPU in turn (on
+    the one-GPU box, all on cuda:0) — and each equals the reference's block."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    import torch
+
+    import xcube_resampling_amd as xrs
+
+    ns = _stub_namespace()
+    jobs = []
+    for case in ("f32", "i16"):
+        g = load_golden(f"reproject_{case}.npz")
+        ds, tgm = reproject_golden_inputs(g)
+        sgm = xrs.GridMapping.from_dataset(ds)
+        plan = xrs.plan_reproject(sgm, tgm, xrs.Transformer.from_crs(tgm.crs, sgm.crs,
+                                                                      always_xy=True))
+        for s in range(g["data"].shape[0]):
+            jobs.append((g, plan, s))
+    jobs = jobs + jobs
+    ngpu = torch.cuda.device_count()
+
+    def block(k):
+        g, plan, s = jobs[k]
+        dev = ns["device_of_block"](k)
+        assert dev.index == k % ngpu
+        out = ns["reproject_tiles"](
+            g["data"][s:s + 1], plan.src_x, plan.src_y, plan.tile_x0, plan.tile_y0,
+            plan.tile_win.reshape(-1), (plan.win_height, plan.win_width),
+            (plan.tile_height, plan.tile_width), (plan.dst_height, plan.dst_width),
+            plan.x_res, plan.y_res, "bilinear", g["fill"].item(), device=dev)
+        exp = g["out_bilinear"][s:s + 1]
+        same = (out == exp) | (np.isnan(out) & np.isnan(exp))
+        return k, out.dtype, exp.dtype, int((~same).sum())
+
+    serial = [block(k) for k in range(len(jobs))]
+    assert all(r[3] == 0 for r in serial), serial
+    with ThreadPoolExecutor(4) as ex:
+        threaded = list(ex.map(block, range(len(jobs))))
+    assert all(r[3] == 0 for r in threaded), threaded

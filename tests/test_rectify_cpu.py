@@ -89,3 +89,23 @@ def test_product_tile_records():
     i_min, j_min, i_max, j_max = bb[1]
     assert (t["si0"], t["sj0"]) == (i_min, j_min)
     assert t["swin"] == min(i_max + 1, g["lon"].shape[1]) - i_min
+
+
+def test_box_grid_decided_on_the_host():
+    """K4's grid mode (and rectify_tiles_device's key scratch) is decided
+    from the boxes alone, before any launch: the tiles of a regular grid
+    qualify; a box list that is not one (or a wrong grid shape) does not."""
+    from xcube_resampling_amd import kernels
+
+    xs = np.array([0.0, 1.0, 2.5, 3.0])
+    ys = np.array([10.0, 9.0, 7.5])
+    boxes = [(xs[i], ys[j + 1], xs[i + 1], ys[j]) for j in range(2) for i in range(3)]
+    b, ntx, nty = kernels._box_grid(boxes, 0.25, (3, 2))
+    assert (ntx, nty) == (3, 2) and b.shape == (6, 4)
+    assert np.array_equal(b[0], [-0.25, 8.75, 1.25, 10.25])
+    assert kernels._box_grid(boxes, 0.25, (2, 3))[1:] == (0, 0)
+    assert kernels._box_grid(boxes, 0.25, (4, 2))[1:] == (0, 0)      # 8 != 6 boxes
+    assert kernels._box_grid(boxes, 0.25, None)[1:] == (0, 0)
+    skew = [list(bx) for bx in boxes]
+    skew[4][0] += 0.1
+    assert kernels._box_grid(skew, 0.0, (3, 2))[1:] == (0, 0)

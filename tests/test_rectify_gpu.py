@@ -438,6 +438,17 @@ def test_k4_filled_claim_keys_equal_in_call_fill():
         assert_bitwise_equal(got, again, run.__name__)
     assert np.isfinite(ij_of(R._device_tiles(sgm, tgm, xy))).mean() > 0.3
 
+    # K5 on a side stream right after K4 + records on the current stream
+    # (ADVICE r04): the records' event orders it, with the K4-filled keys
+    ref = ij_of(R._device_tiles(sgm, tgm, xy))
+    side = torch.cuda.Stream()
+    for _ in range(3):
+        t = R._device_tiles(sgm, tgm, xy)
+        out = kernels.rectify_ij(xy[0], xy[1], t, 0, tgm.height, tgm.width, tgm.x_res,
+                                 -tgm.y_res, 1e-3, stream=side)
+        side.synchronize()
+        assert_bitwise_equal(out.cpu().numpy(), ref, "side stream")
+
     # the fill: odd word counts (16-byte body + tail), accumulators as without
     boxes = np.asarray(tgm.xy_bboxes, np.float64)
     grid = (len(range(0, tgm.width, tgm.tile_width)), len(range(0, tgm.height, tgm.tile_height)))
@@ -523,8 +534,10 @@ def test_claim_fast_decisions_equal_exact_divisions():
 def test_config4_full_size_matches_oracle():
     """BASELINE config 4 at full size: the 4000x4800 jittered swath (f64
     lon/lat) rectified to the ~8266x5392 EPSG:4326 grid in 512^2 tiles — K4
-    bboxes, K5 source positions and K6 samples (nearest, bilinear) == the C
-    oracle of the numba kernels on the whole swath, bit for bit."""
+    bboxes, K5 source positions and K6 samples (nearest, bilinear,
+    triangular — rectify.py:663-734), unfused and fused into the resolve pass
+    with and without the ij image, == the C oracle of the numba kernels on
+    the whole swath, bit for bit."""
     import torch
 
     from oracle import gridmapping_ref as gref
@@ -561,7 +574,7 @@ def test_config4_full_size_matches_oracle():
                                       xrs.DataArray(lat, ("y", "x"), name="lat"), "EPSG:4326")
     xy = (torch.from_numpy(lon).cuda(), torch.from_numpy(lat).cuda())
     dev_tiles = R._device_tiles(sgm, tgm, xy)
-    for interp in ("nearest", "bilinear"):
+    for interp in ("nearest", "bilinear", "triangular"):
         exp = rectify_ref.compute_var_image(exp_ij, var, np.nan, interp, tile, threads=16)
         assert_bitwise_equal(kernels.rectify_var(ij, src, interp, np.nan).cpu().numpy(), exp,
                              interp)

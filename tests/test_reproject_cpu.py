@@ -138,3 +138,61 @@ def test_non_separable_plan_fuses_only_above_table_budget():
     assert sep.coord_mode == 0
     with xrs.set_options(reproject_table_max_bytes=0):
         assert not sep.fused_transform("cuda:0")
+
+
+@pytest.mark.parametrize("size,tile,crs_pair", [
+    ((900, 700), (128, 96), ("EPSG:3857", "EPSG:4326")),     # partial last tile column
+    ((4096, 512), (2048, 512), ("EPSG:3857", "EPSG:4326")),
+    ((1000, 300), (1000, 300), ("EPSG:4326", "EPSG:3857")),  # one tile column, forward webmerc
+    ((777, 65), (64, 65), ("EPSG:4326", "EPSG:4326")),        # identity
+    ((513, 40), (64, 40), ("EPSG:3857", "EPSG:4326")),       # a last block of one column
+])
+def test_column_generators_reproduce_src_x(size, tile, crs_pair):
+    """coord_mode 2 (K1 computes its column coordinates): the records
+    reproduce the plan's src_x bit for bit on regular target grids — dask's
+    blockwise linspace per tile column, then the separable transformation's
+    scalings — and are refused (None) the moment one column differs."""
+    import xcube_resampling_amd as xrs
+    from xcube_resampling_amd.reproject import column_generators
+
+    tcrs, scrs = crs_pair
+    xmin = -500000.0 if tcrs == "EPSG:3857" else -4.25
+    res = 800.0 if tcrs == "EPSG:3857" else 0.0071
+    tgm = xrs.GridMapping.regular(size, (xmin, 6500000.0 if tcrs == "EPSG:3857" else 50.0),
+                                  res, tcrs, tile_size=tile)
+    tr = xrs.Transformer.from_crs(tgm.crs, scrs, always_xy=True)
+    tx = tgm.x_coords.values
+    src_x = tr.transform_x(tx)
+    recs = column_generators(tx, tile[0], src_x, tr.separable_x_scales())
+    assert recs is not None and recs.shape == (4 * -(-size[0] // tile[0]) + 2,)
+    # the kernel's evaluation, restated
+    m1, m2 = recs[-2:]
+    got = np.empty_like(src_x)
+    for c in range(size[0]):
+        tx_i, k = divmod(c, tile[0])
+        start, stop, step, n = recs[4 * tx_i:4 * tx_i + 4]
+        v = stop if k == int(n) - 1 else k * step + start
+        got[c] = (v * m1) * m2
+    assert_bitwise_equal(got, src_x)
+    bad = src_x.copy()
+    bad[size[0] // 2] = np.nextafter(bad[size[0] // 2], np.inf)
+    assert column_generators(tx, tile[0], bad, tr.separable_x_scales()) is None
+    assert column_generators(tx, tile[0], src_x, None) is None
+
+
+def test_reproject_plans_use_column_generators():
+    """The bench workload (config 5) and the golden plans qualify for
+    coord_mode 2; a non-separable plan has no generators."""
+    import xcube_resampling_amd as xrs
+
+    g = load_golden("reproject_f32.npz")
+    ds, tgm = reproject_golden_inputs(g)
+    sgm = xrs.GridMapping.from_dataset(ds)
+    plan = xrs.plan_reproject(sgm, tgm, xrs.Transformer.from_crs(tgm.crs, sgm.crs,
+                                                                  always_xy=True))
+    assert plan.coord_mode == 0 and plan.x_gen is not None
+    utm = xrs.GridMapping.regular((64, 48), (500000.0, 5500000.0), 100.0, "EPSG:32632",
+                                  tile_size=32)
+    plan2 = xrs.plan_reproject(sgm, utm, xrs.Transformer.from_crs(utm.crs, sgm.crs,
+                                                                   always_xy=True))
+    assert plan2.coord_mode == 1 and plan2.x_gen is None

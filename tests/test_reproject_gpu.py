@@ -47,7 +47,11 @@ def test_work_shapes_are_bit_identical(band, bpc):
     resolve of the row entries covers (65-200 rows: the entries are resolved
     again every 64 rows) — all reproduce the reference bit for bit.  The
     shapes are forced through the test-only knobs (xrs_testing_set); the
-    product never reads them from the environment."""
+    product never reads them from the environment.  Each shape runs with the
+    column coordinates generated in the kernel (coord_mode 2) and read from
+    the src_x table (coord_mode 0)."""
+    import dataclasses
+
     import torch
 
     import xcube_resampling_amd as xrs
@@ -60,13 +64,17 @@ def test_work_shapes_are_bit_identical(band, bpc):
         sgm = xrs.GridMapping.from_dataset(ds)
         plan = xrs.plan_reproject(sgm, tgm, xrs.Transformer.from_crs(tgm.crs, sgm.crs,
                                                                       always_xy=True))
+        assert plan.x_gen is not None
+        # coord_mode 2 (column generators) and 0 (the src_x table)
+        table = dataclasses.replace(plan, x_gen=None, _device_cache={})
         src = torch.from_numpy(g["data"]).cuda()
         for interp in ("nearest", "bilinear", "triangular"):
-            with testing_knob("reproject_band", band), \
-                    testing_knob("reproject_blocks_per_cu", bpc):
-                out = kernels.reproject(src, plan, interp, g["fill"].item())
-            assert_bitwise_equal(out.cpu().numpy(), g[f"out_{interp}"],
-                                 f"{case}/{interp} band={band} bpc={bpc}")
+            for p, mode in ((plan, "gen"), (table, "table")):
+                with testing_knob("reproject_band", band), \
+                        testing_knob("reproject_blocks_per_cu", bpc):
+                    out = kernels.reproject(src, p, interp, g["fill"].item())
+                assert_bitwise_equal(out.cpu().numpy(), g[f"out_{interp}"],
+                                     f"{case}/{interp} band={band} bpc={bpc} {mode}")
 
 
 @pytest.mark.parametrize("case", NO_DOWNSCALE)

@@ -97,3 +97,49 @@ def test_band_rows_multiple_of_unit():
     assert _band_rows(1000, 1 << 20, 8) % 8 == 0
     assert _band_rows(10, 1, 8) == 16     # whole (rounded-up) height in one band
     assert _band_rows(5000, 64 << 20, 7) == 7
+
+
+def test_staging_pool_is_bounded_and_exclusive(monkeypatch):
+    """staging pairs are borrowed from a process-wide pool of at
+    most _POOL_MAX, one thread at a time each, and returned drained — not one
+    pinned pair per thread for the thread's life."""
+    import threading
+    import time
+
+    from xcube_resampling_amd import streaming
+
+    made, in_use, peak = [], set(), [0]
+    lock = threading.Lock()
+
+    class FakeStaging:
+        def __init__(self):
+            made.append(self)
+            self.drained = 0
+
+        def drain(self):
+            self.drained += 1
+
+    monkeypatch.setattr(streaming, "_Staging", FakeStaging)
+    monkeypatch.setattr(streaming, "_POOL_FREE", [])
+    monkeypatch.setattr(streaming, "_POOL_MADE", 0)
+    monkeypatch.setattr(streaming, "_POOL_MAX", 3)
+
+    def work(_):
+        for _ in range(5):
+            with streaming._staging() as st:
+                with lock:
+                    assert st not in in_use          # never shared by two threads
+                    in_use.add(st)
+                    peak[0] = max(peak[0], len(in_use))
+                time.sleep(0.002)
+                with lock:
+                    in_use.discard(st)
+
+    ts = [threading.Thread(target=work, args=(k,)) for k in range(12)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert len(made) <= 3 and peak[0] <= 3
+    assert sorted(map(id, streaming._POOL_FREE)) == sorted(map(id, made))
+    assert sum(s.drained for s in made) == 12 * 5

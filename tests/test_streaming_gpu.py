@@ -237,14 +237,18 @@ def test_staging_round_trip_multi_chunk():
             back = streaming.device_to_host(d)
             assert back.dtype == a.dtype
             assert np.array_equal(back.view(np.uint8), np.ascontiguousarray(a).view(np.uint8))
-    assert streaming._staging() is streaming._staging()
-    assert len(streaming._staging().bufs) == 2
+    with streaming._staging() as a:
+        assert len(a.bufs) == 2
+    with streaming._staging() as b:      # a drained pair is handed out again
+        assert b is a
 
 
 def test_staging_concurrent_threads():
     """Streamed copies from several host threads at once (a threaded chunk
-    scheduler calling the dataset APIs): each thread stages through its own
-    page-locked pair, so no thread's bytes land in another's array."""
+    scheduler calling the dataset APIs): a thread borrows a page-locked pair
+    from the pool for each transfer, so no thread's bytes land in another's
+    array, and the pool never holds more than _POOL_MAX pairs (ADVICE r04:
+    no pinned pair per thread for the life of the thread)."""
     from concurrent.futures import ThreadPoolExecutor
 
     import torch
@@ -265,12 +269,13 @@ def test_staging_concurrent_threads():
         for _ in range(3):
             d = streaming.host_to_device(a, "cuda:0")
             ok &= np.array_equal(streaming.device_to_host(d), a)
-        return ok, id(streaming._staging())
+        return ok
 
     with set_options(host_streaming_min_bytes=0), ThreadPoolExecutor(4) as ex:
         res = list(ex.map(work, range(4)))
-    assert all(ok for ok, _ in res)
-    assert len({i for _, i in res}) == 4
+    assert all(res)
+    assert 1 <= streaming._POOL_MADE <= streaming._POOL_MAX
+    assert len(streaming._POOL_FREE) == streaming._POOL_MADE   # every pair returned
 
 
 def test_host_register_copy_unregister_then_fresh_pageable_copy():

@@ -18,7 +18,7 @@ from dataclasses import dataclass, field
 
 import numpy as np
 
-from . import _native, kernels
+from . import _native, kernels, multidevice
 from .dataset import DataArray, Dataset
 from .device import is_device_array, require_device, to_device
 from . import streaming
@@ -289,6 +289,12 @@ def _resample_array(data, dims, chunks, affine_matrix, output_shape, output_chun
     if len(data.shape) > 3:
         raise NotImplementedError("the engine resamples 2-D and 3-D variables")
     device = require_device()
+    devices = multidevice.active_devices()
+    if devices is not None:
+        res = _resample_partitioned(data, affine_matrix, output_shape, output_chunks, interp,
+                                    agg, recover_nan, fill_value, devices)
+        if res is not None:
+            return res
     if isinstance(data, np.ndarray) and data.ndim in (2, 3) and \
             data.nbytes >= get_options()["host_streaming_min_bytes"] and \
             not (recover_nan and interp > 0 and np.issubdtype(data.dtype, np.floating)):
@@ -319,10 +325,87 @@ def _resample_array(data, dims, chunks, affine_matrix, output_shape, output_chun
     return out[0] if expanded else out
 
 
+def _resample_partitioned(data, affine_matrix, output_shape, output_chunks, interp, agg,
+                          recover_nan, fill_value, devices):
+    """K2 / K3 over several devices (``multidevice``): output chunk row bands
+    (``sharding.coarsen_shard``), each device holding only the source rows its
+    chunks' dask-image footprints read (affine.py:336-343: the footprint
+    carries the order-1 halo and the NaN dilation), one host thread and
+    stream per device.  ``da.any(mask)`` (affine.py:347-349) is the whole
+    array's: every device tests its rows, the rows no band reads are tested
+    too.  Returns None for plans that cannot be split (a separate coarsen
+    pass, chunks without whole windows, uint64 sums): those run whole on the
+    current device."""
+    from .sharding import coarsen_shard
+
+    expanded = data.ndim == 2
+    on_device = is_device_array(data)
+    arr = (data.unsqueeze(0) if on_device else np.asarray(data).reshape((1,) + data.shape)) \
+        if expanded else (data if on_device else np.asarray(data))
+    if on_device:
+        from .device import numpy_dtype
+        dtype = numpy_dtype(arr.dtype)
+    else:
+        dtype = np.dtype(arr.dtype)
+    shape = tuple(arr.shape)
+    plan = plan_affine(shape, dtype, affine_matrix, output_shape, output_chunks, interp, agg,
+                       False, fill_value)
+    if plan.post_agg is not None or plan.chunk_y % plan.div_y != 0 or \
+            np.dtype(plan.out_dtype) == np.uint64:
+        return None
+    world = len(devices)
+    shards = [coarsen_shard(plan, world, i) for i in range(world)]
+
+    def upload(i, dev):
+        sh = shards[i]
+        if sh.chunk1 <= sh.chunk0:
+            return None
+        return multidevice.rows_to_device(arr, sh.src_row0, sh.src_row1, dev)
+
+    bands = multidevice.run_parts(devices, upload, sources=[arr])
+    if recover_nan and interp > 0 and np.issubdtype(dtype, np.floating):
+        if on_device:
+            recover = kernels.any_nan(arr.contiguous())
+        else:
+            def test(i, dev):
+                return bands[i] is not None and kernels.any_nan(bands[i].contiguous())
+            recover = any(multidevice.run_parts(devices, test))
+            if not recover:   # rows no band reads are part of the reference's test
+                read = np.zeros(shape[1], bool)
+                for sh in shards:
+                    read[sh.src_row0:sh.src_row1] = True
+                rest = np.flatnonzero(~read)
+                if rest.size:
+                    recover = kernels.any_nan(host_to_device(
+                        np.ascontiguousarray(arr[:, rest]), require_device()))
+        if recover:
+            plan = plan_affine(shape, dtype, affine_matrix, output_shape, output_chunks, interp,
+                               agg, True, fill_value)
+            shards = [coarsen_shard(plan, world, i) for i in range(world)]
+    out = multidevice.output_like(arr, (shape[0], plan.out_h, plan.out_w), plan.out_dtype)
+
+    def part(i, dev):
+        sh = shards[i]
+        if bands[i] is None:
+            return
+        res = kernels.affine(bands[i], sh.plan)
+        multidevice.put_rows(out, sh.row0, sh.row1, res)
+
+    multidevice.run_parts(devices, part)
+    return out[0] if expanded else out
+
+
 def resample_dataset(dataset, affine_matrix, yx_dims: tuple[str, str], target_size,
                      target_tile_size, interp_methods=None, agg_methods=None,
-                     recover_nans=False, fill_values=None) -> Dataset:
-    """affine.py:140-240."""
+                     recover_nans=False, fill_values=None, devices=None) -> Dataset:
+    """affine.py:140-240 (``devices``: see affine_transform_dataset)."""
+    with multidevice.use_devices(devices):
+        return _resample_dataset(dataset, affine_matrix, yx_dims, target_size, target_tile_size,
+                                 interp_methods, agg_methods, recover_nans, fill_values)
+
+
+def _resample_dataset(dataset, affine_matrix, yx_dims, target_size, target_tile_size,
+                      interp_methods, agg_methods, recover_nans, fill_values) -> Dataset:
     dataset = as_dataset(dataset)
     data_vars, coords = {}, {}
     for var_name, data_array in dataset.variables.items():
@@ -359,8 +442,17 @@ def resample_dataset(dataset, affine_matrix, yx_dims: tuple[str, str], target_si
 def affine_transform_dataset(source_ds, target_gm: GridMapping,
                              source_gm: GridMapping | None = None,
                              variables: str | Iterable[str] | None = None, interp_methods=None,
-                             agg_methods=None, recover_nans=False, fill_values=None) -> Dataset:
-    """affine.py:52-137."""
+                             agg_methods=None, recover_nans=False, fill_values=None,
+                             devices=None) -> Dataset:
+    """affine.py:52-137.  ``devices`` (engine extension): split every
+    variable's output chunk rows over these GPUs (``multidevice``)."""
+    with multidevice.use_devices(devices):
+        return _affine_transform_dataset(source_ds, target_gm, source_gm, variables,
+                                         interp_methods, agg_methods, recover_nans, fill_values)
+
+
+def _affine_transform_dataset(source_ds, target_gm, source_gm, variables, interp_methods,
+                              agg_methods, recover_nans, fill_values) -> Dataset:
     source_ds = as_dataset(source_ds)
     if source_gm is None:
         source_gm = GridMapping.from_dataset(source_ds)
@@ -370,7 +462,7 @@ def affine_transform_dataset(source_ds, target_gm: GridMapping,
         f"{source_gm.crs.name!r} and target CRS {target_gm.crs.name!r}"
     )
     source_ds = _select_variables(source_ds, variables)
-    target_ds = resample_dataset(
+    target_ds = _resample_dataset(
         source_ds, target_gm.ij_transform_to(source_gm),
         (source_gm.xy_dim_names[1], source_gm.xy_dim_names[0]), target_gm.size,
         target_gm.tile_size, interp_methods, agg_methods, recover_nans, fill_values)

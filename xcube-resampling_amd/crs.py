@@ -528,6 +528,23 @@ class Transformer:
         Mercator); other pairs need 2-D coordinate tables."""
         return self._separable
 
+    def separable_x_scales(self):
+        """(m1, m2) with x' = (x * m1) * m2 in this transformer's operation
+        order, for the separable pipelines made of scalings (identity,
+        geographic <-> geographic, web Mercator inverse or forward; PROJ
+        webmerc's x: ``lam = x * ra`` then the rad -> deg factor, or
+        ``a * (lon * deg -> rad)``); None otherwise.  Used only through
+        reproject.column_generators, which checks the result bit for bit."""
+        if not self._separable:
+            return None
+        if not self._step_crs:
+            return (1.0, 1.0)
+        if len(self._step_crs) == 1 and self._step_crs[0][0].kind == "webmerc":
+            if self._step_crs[0][1]:
+                return (1.0 / _WGS84_A, _RAD_TO_DEG_FACTOR)
+            return (_DEG_TO_RAD, _WGS84_A)
+        return None
+
     def device_steps(self):
         """The pipeline as a ctypes array of XrsProjStep records for
         xrs_transform (kernels.transform)."""

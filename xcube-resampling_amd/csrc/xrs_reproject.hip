@@ -72,6 +72,17 @@ struct AxisEntry {   // one resolved column (or row) of one tile
 };
 static_assert(sizeof(AxisEntry) == 16, "AxisEntry layout");
 
+// coord_mode 2: the source-CRS x of target column c in tile column tx, as the
+// host computes it (dask's blockwise linspace of the pixel centres,
+// regular.py:44-52, then the separable transformation's scalings,
+// reproject.py:472-496): v = k == n-1 ? stop : k * step + start (k = c - tx *
+// tile_w), x = (v * m1) * m2.  src_x then holds ntiles_x records followed by
+// (m1, m2); the host uses this mode only after checking it bit for bit.
+struct ColumnGen {
+  double start, stop, step, n;
+};
+static_assert(sizeof(ColumnGen) == 32, "ColumnGen layout");
+
 struct Geometry {
   int64_t src_h, src_w, src_row0, src_rows;
   int64_t dst_h, dst_w, row_begin, row_end;
@@ -87,6 +98,7 @@ struct Geometry {
   int64_t band;   // target rows per work item of the gathers
   int64_t segw;   // target columns per work item (kThreads x columns per thread)
   int64_t band_first;   // bands of tile row ty0 above row_begin (not in the work list)
+  int64_t xgen;         // K1b: src_x holds column generators (coord_mode 2, ColumnGen)
 };
 
 // numpy fancy index on a window axis of length `win` with an int16 index:
@@ -242,15 +254,35 @@ gather_separable_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t bands_
     WorkItem it;
     if (!work_item(g, w, ty0, nsegs, bands_per_tile, segs_per_tile, it)) continue;
     const int ncols = (int)(it.c1 - it.c0);
-    // this item's columns: coordinates requested together, then resolved
+    // this item's columns and its first 64 rows: the source-CRS coordinates
+    // are requested together (one memory round trip before the taps), then
+    // resolved
     const float x0 = g.tile_x0[it.t];
     const int64_t wi0 = g.tile_win[2 * it.t];
+    const float y0 = g.tile_y0[it.t];
+    const int64_t wj0 = g.tile_win[2 * it.t + 1];
     double sx[kPx];
+    if (g.xgen) {
+      // coord_mode 2: the column coordinates from the tile column's
+      // generator — the host checked it reproduces src_x bit for bit
+      const ColumnGen cg = reinterpret_cast<const ColumnGen*>(g.src_x)[it.tx];
+      const double m1 = g.src_x[4 * g.ntiles_x], m2 = g.src_x[4 * g.ntiles_x + 1];
+      const int last = (int)cg.n - 1, k0 = (int)(it.c0 - it.tx * g.tile_w);
 #pragma unroll
-    for (int k = 0; k < kPx; ++k) {
-      const int lc = (int)threadIdx.x + k * kThreads;
-      sx[k] = g.src_x[it.c0 + min(lc, ncols - 1)];
+      for (int k = 0; k < kPx; ++k) {
+        const int kk = k0 + min((int)threadIdx.x + k * kThreads, ncols - 1);
+        const double v = kk == last ? cg.stop : (double)kk * cg.step + cg.start;
+        sx[k] = (v * m1) * m2;
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < kPx; ++k) {
+        const int lc = (int)threadIdx.x + k * kThreads;
+        sx[k] = g.src_x[it.c0 + min(lc, ncols - 1)];
+      }
     }
+    const int64_t ry0 = it.r0 + lane;
+    const double sy0 = g.src_y[min(ry0, it.r1 - 1)];
     int32_t cf[kPx], cc[kPx];
     double dx[kPx];
 #pragma unroll
@@ -273,11 +305,16 @@ gather_separable_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t bands_
     }
     // this item's rows: lane q holds the entry of row ybase + q (rows past
     // r1 hold "outside", as the batches expect); one resolve per 64 rows
-    const float y0 = g.tile_y0[it.t];
-    const int64_t wj0 = g.tile_win[2 * it.t + 1];
     int32_t yf = -1, yc = -1;
     double yd = 0.0;
-    int64_t ybase = it.r0 - 64;
+    int64_t ybase = it.r0;
+    if (ry0 < it.r1) {
+      const AxisEntry e = resolve_axis<INTERP>(sy0, y0, g.neg_y_res, g.win_h, wj0, g.src_h,
+                                               g.src_row0, g.src_rows, eflags);
+      yf = e.f;
+      yc = e.c;
+      yd = e.d;
+    }
     for (int64_t sn = 0; sn < a.n; ++sn) {
       const T* __restrict__ src = static_cast<const T*>(a.src) + sn * a.src_sn;
       O* __restrict__ dst = static_cast<O*>(a.dst) + sn * a.dst_sn - g.row_begin * a.dst_sy + it.c0;
@@ -629,8 +666,8 @@ inline Work work_of(const GatherArgs& a, int64_t band = kBand, int64_t segw = kS
 
 template <typename T, typename O, int INTERP>
 int launch(const GatherArgs& a, int coord_mode, hipStream_t stream) {
-  Work k = coord_mode == 0 ? work_of(a, K1Shape<O>::band, K1Shape<O>::segw) : work_of(a);
-  if (coord_mode == 0) {
+  Work k = coord_mode != 1 ? work_of(a, K1Shape<O>::band, K1Shape<O>::segw) : work_of(a);
+  if (coord_mode != 1) {
     hipLaunchKernelGGL((gather_separable_kernel<T, O, INTERP>), dim3(k.nb), dim3(kThreads), 0,
                        stream, k.args, k.ty0, k.nsegs, k.bands_per_tile, k.segs_per_tile, k.nwork);
   } else {
@@ -725,7 +762,7 @@ extern "C" int xrs_reproject(const void* src, int src_dtype, int64_t n, int64_t 
       n < 1 || src_h < 1 || src_w < 1 || dst_h < 1 || dst_w < 1 || tile_h < 1 || tile_w < 1 ||
       win_h < 1 || win_w < 1 || row_begin < 0 || row_end > dst_h || row_begin > row_end ||
       src_rows < 0 || src_sy < src_w || src_w > INT32_MAX || src_rows > INT32_MAX ||
-      (coord_mode != 0 && coord_mode != 1)) {
+      coord_mode < 0 || coord_mode > 2) {
     xrs_set_error("xrs_reproject: invalid argument");
     return XRS_ERR_ARG;
   }
@@ -760,6 +797,7 @@ extern "C" int xrs_reproject(const void* src, int src_dtype, int64_t n, int64_t 
   g.src_x = src_x; g.src_y = src_y; g.tile_x0 = tile_x0; g.tile_y0 = tile_y0;
   g.tile_win = tile_win; g.win_h = win_h; g.win_w = win_w;
   g.x_res = x_res; g.neg_y_res = -y_res; g.err_flags = err_flags; g.band = kBand; g.segw = kSegW; g.band_first = 0;
+  g.xgen = coord_mode == 2;
   a.src = src; a.n = n; a.src_sn = src_sn; a.src_sy = src_sy;
   a.dst = dst; a.dst_sn = dst_sn; a.dst_sy = dst_sy; a.fill = fill;
   hipStream_t st = static_cast<hipStream_t>(stream);
@@ -840,6 +878,7 @@ extern "C" int xrs_reproject_proj(const void* src, int src_dtype, int64_t n, int
   g.src_x = grid_x; g.src_y = grid_y; g.tile_x0 = tile_x0; g.tile_y0 = tile_y0;
   g.tile_win = tile_win; g.win_h = win_h; g.win_w = win_w;
   g.x_res = x_res; g.neg_y_res = -y_res; g.err_flags = err_flags; g.band = kBand; g.segw = kSegW; g.band_first = 0;
+  g.xgen = 0;
   a.src = src; a.n = n; a.src_sn = src_sn; a.src_sy = src_sy;
   a.dst = dst; a.dst_sn = dst_sn; a.dst_sy = dst_sy; a.fill = fill;
   XrsProjStep s0{}, s1{};

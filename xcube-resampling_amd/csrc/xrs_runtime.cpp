@@ -79,13 +79,25 @@ extern "C" int xrs_host_unregister(void* ptr) {
     xrs_set_error("xrs_host_unregister: invalid argument");
     return XRS_ERR_ARG;
   }
-  // A copy queued on any stream (the band pipelines use three) may still
-  // read or write the range: drain the device before the pages are unpinned,
-  // so no DMA outlives the registration it was issued under.
-  hipError_t e = hipDeviceSynchronize();
+  // A copy queued on any stream of any device (the band pipelines use three
+  // streams, a multi-GPU process one or more per device) may still read or
+  // write the range: drain every visible device before the pages are
+  // unpinned, so no DMA outlives the registration it was issued under.  (A
+  // binding that knows the streams should synchronise those and keep the
+  // registration out of graph-capture windows: a device drain stalls
+  // unrelated work, include/xrs.h.)
+  int ndev = 0, cur = 0;
+  hipError_t e = hipGetDeviceCount(&ndev);
+  if (e == hipSuccess) e = hipGetDevice(&cur);
+  for (int d = 0; e == hipSuccess && d < ndev; ++d) {
+    e = hipSetDevice(d);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+  }
+  const hipError_t er = hipSetDevice(cur);
+  if (e == hipSuccess) e = er;
   if (e != hipSuccess) {
     (void)hipGetLastError();
-    xrs_set_error("xrs_host_unregister: hipDeviceSynchronize: %s", hipGetErrorString(e));
+    xrs_set_error("xrs_host_unregister: draining the devices: %s", hipGetErrorString(e));
     return XRS_ERR_HIP;
   }
   e = hipHostUnregister(ptr);

@@ -93,11 +93,14 @@ def reproject(src, plan, interp: str, fill: float, out_dtype=None, rows=None, ou
     dn, dy, dx = out.stride()
     if sx != 1 or dx != 1:
         raise ValueError("innermost dimension must be contiguous")
+    # coord_mode 2: the separable plan's column coordinates generated in K1
+    gen = plan.coord_mode == 0 and "x_gen" in tables
     rc = lib.xrs_reproject(
         ptr(src), src_dtype, n, plan.src_height, plan.src_width, src_row0, h_band, sn, sy,
         ptr(out), _native.dtype_code(out_dtype), plan.dst_height, plan.dst_width, r0, r1,
         dn, dy, plan.tile_height, plan.tile_width,
-        ptr(tables["src_x"]), ptr(tables["src_y"]), plan.coord_mode,
+        ptr(tables["x_gen"] if gen else tables["src_x"]), ptr(tables["src_y"]),
+        2 if gen else plan.coord_mode,
         ptr(tables["tile_x0"]), ptr(tables["tile_y0"]), ptr(tables["tile_win"]),
         plan.win_height, plan.win_width, float(plan.x_res), float(plan.y_res),
         interp_code, float(fill), ptr(ws) if ws is not None else None, ws_bytes, flags.ptr,
@@ -160,6 +163,24 @@ def _upload_small(arr: np.ndarray, device, stream):
     return to_device(np.ascontiguousarray(arr), device)
 
 
+def _box_grid(xy_bboxes, xy_border, grid):
+    """(bordered boxes (n, 4), ntx, nty): the boxes with the border applied
+    (bboxes.py:60-63), and the grid shape when they are the tiles of a
+    regular grid — every tile column shares its x bounds and every tile row
+    its y bounds — else (0, 0) (K4 then tests every box)."""
+    boxes = np.asarray(xy_bboxes, dtype=np.float64).reshape(-1, 4)
+    b = np.stack([boxes[:, 0] - xy_border, boxes[:, 1] - xy_border,
+                  boxes[:, 2] + xy_border, boxes[:, 3] + xy_border], axis=1)
+    if grid is not None:
+        ntx, nty = grid
+        if ntx * nty == b.shape[0]:
+            bb = b.reshape(nty, ntx, 4)
+            if np.all(bb[:, :, [0, 2]] == bb[:1, :, [0, 2]]) and \
+                    np.all(bb[:, :, [1, 3]] == bb[:, :1, [1, 3]]):
+                return b, ntx, nty
+    return b, 0, 0
+
+
 def _ij_bboxes_launch(x_image, y_image, xy_bboxes, xy_border, grid, device, stream, fill=None):
     """Launch K4; returns (device int32 accumulators (n, 4), n, (w, h), grid
     mode used).  ``fill``: a contiguous 4-byte tensor K4's grid sets to ~0
@@ -168,18 +189,10 @@ def _ij_bboxes_launch(x_image, y_image, xy_bboxes, xy_border, grid, device, stre
     x = to_device(x_image, device, np.float64)
     y = to_device(y_image, device, np.float64)
     h, w = x.shape
-    boxes = np.asarray(xy_bboxes, dtype=np.float64).reshape(-1, 4)
-    n = boxes.shape[0]
-    # bboxes.py:60-63 (the border is applied to every box before comparing)
-    b = np.stack([boxes[:, 0] - xy_border, boxes[:, 1] - xy_border,
-                  boxes[:, 2] + xy_border, boxes[:, 3] + xy_border], axis=1)
-    ntx = nty = 0
-    if grid is not None:
-        ntx, nty = grid
+    b, ntx, nty = _box_grid(xy_bboxes, xy_border, grid)
+    n = b.shape[0]
+    if ntx > 0:
         bb = b.reshape(nty, ntx, 4)
-        if not (ntx * nty == n and np.all(bb[:, :, [0, 2]] == bb[:1, :, [0, 2]]) and
-                np.all(bb[:, :, [1, 3]] == bb[:, :1, [1, 3]])):
-            ntx = nty = 0
     # one upload for the boxes and the accumulators' initial values (each
     # small copy is a blit of ~6 us on the stream ahead of K4): float64 box
     # bounds first, the int32 (i_min, j_min, i_max, j_max) after them
@@ -245,10 +258,19 @@ class DeviceTiles:
     them.  The scratch serves the first K5 call given these tiles (its claim
     pass consumes the fill); later calls fill their own."""
 
-    __slots__ = ("tiles", "offs", "_keys")
+    __slots__ = ("tiles", "offs", "_keys", "ready", "made_on")
 
-    def __init__(self, tiles, offs, keys):
+    def __init__(self, tiles, offs, keys, ready=None, made_on=None):
         self.tiles, self.offs, self._keys = tiles, offs, keys
+        self.ready = ready       # event after K4 + xrs_rectify_tiles ...
+        self.made_on = made_on   # ... on this stream (handle)
+
+    def wait(self, stream) -> None:
+        """Order `stream` after the launches that made these records and
+        filled the key scratch, when they ran on another stream (on the same
+        stream the order is given)."""
+        if self.ready is not None and int(stream.cuda_stream) != self.made_on:
+            stream.wait_event(self.ready)
 
     def __iter__(self):
         return iter((self.tiles, self.offs))
@@ -268,11 +290,12 @@ def rectify_tiles_device(x_image, y_image, target_xy_bboxes, xy_border: float, i
     Returns a DeviceTiles (K4 also fills the K5 claim-key scratch), or None
     when the boxes are not a regular tile grid."""
     dev = require_device(device if device is not None else getattr(x_image, "device", None))
+    if _box_grid(target_xy_bboxes, xy_border, grid)[1] == 0:
+        return None   # decided on the host: no K4 launch, no key scratch (ADVICE r04)
     keys = torch().empty((dst_size[1], dst_size[0]), dtype=torch().int32, device=dev)
     acc, n, (w, h), is_grid = _ij_bboxes_launch(x_image, y_image, target_xy_bboxes, xy_border,
                                                 grid, device, stream, fill=keys)
-    if not is_grid:
-        return None
+    assert is_grid
     device = acc.device
     ntx, nty = grid
     tiles = torch().empty(n * TILE_INFO_DTYPE.itemsize, dtype=torch().uint8, device=device)
@@ -284,7 +307,10 @@ def rectify_tiles_device(x_image, y_image, target_xy_bboxes, xy_border: float, i
         float(dst_res[1]), int(bool(j_axis_up)), ptr(tiles), ptr(offs),
         stream_handle(device, stream))
     _native.check(rc, "xrs_rectify_tiles")
-    return DeviceTiles(tiles, offs, keys)
+    s = stream if stream is not None else torch().cuda.current_stream(device)
+    ready = torch().cuda.Event()
+    ready.record(s)
+    return DeviceTiles(tiles, offs, keys, ready, int(s.cuda_stream))
 
 
 def transform(transformer, x, y, grid: bool, device=None, stream=None):
@@ -337,9 +363,10 @@ def _claim_keys(tiles, dst_h, dst_w, device):
     return torch().empty((dst_h, dst_w), dtype=torch().int32, device=device), 0
 
 
-def _rect_inputs(x_image, y_image, tiles, device):
+def _rect_inputs(x_image, y_image, tiles, device, stream=None):
     """Device x/y images, tile records, chunk offsets and the strip count
-    of a K5 call (host tiles get their offsets computed here)."""
+    of a K5 call (host tiles get their offsets computed here).  Device tiles
+    made on another stream are waited for on the K5 stream."""
     x = to_device(x_image, device, np.float64)
     y = to_device(y_image, device, np.float64)
     if isinstance(tiles, np.ndarray):   # host tiles: offsets computed here
@@ -352,6 +379,8 @@ def _rect_inputs(x_image, y_image, tiles, device):
     else:                                 # device tiles from rectify_tiles_device
         t_dev, offs = tiles
         ntiles, max_chunks = offs.numel() - 1, 0
+        if isinstance(tiles, DeviceTiles):
+            tiles.wait(stream if stream is not None else torch().cuda.current_stream(device))
     return x, y, t_dev, offs, ntiles, max_chunks
 
 
@@ -369,7 +398,7 @@ def rectify_ij(x_image, y_image, tiles: np.ndarray, ntiles_x: int, dst_h: int, d
     sharding.rectify_shard): pixels of the other tiles are NaN, not garbage.
     """
     device = require_device(device)
-    x, y, t_dev, offs, ntiles, max_chunks = _rect_inputs(x_image, y_image, tiles, device)
+    x, y, t_dev, offs, ntiles, max_chunks = _rect_inputs(x_image, y_image, tiles, device, stream)
     h, w = x.shape
     keys, keys_ready = _claim_keys(tiles, dst_h, dst_w, device)
     ij = (torch().full((2, dst_h, dst_w), float("nan"), dtype=torch().float64, device=device)
@@ -405,7 +434,7 @@ def rectify_ij_var(x_image, y_image, tiles, dst_h: int, dst_w: int, x_scale: flo
             f"'triangular', was '{interp}'.")
     if src.dim() != 3 or src.stride(2) != 1:
         raise ValueError("src must be (n, H, W) with contiguous rows")
-    x, y, t_dev, offs, ntiles, max_chunks = _rect_inputs(x_image, y_image, tiles, device)
+    x, y, t_dev, offs, ntiles, max_chunks = _rect_inputs(x_image, y_image, tiles, device, stream)
     h, w = x.shape
     n, sh, sw = src.shape
     keys, keys_ready = _claim_keys(tiles, dst_h, dst_w, device)
@@ -467,19 +496,28 @@ def rectify_var(ij, src, interp: str, fill, stream=None, rows=None, out=None,
 _WORKSPACES: dict = {}
 
 
-def _workspace(device, nbytes: int):
-    key = str(device)
+def _workspace(device, nbytes: int, stream=None):
+    """K2/K3's scratch for launches on `stream` (default: the current stream),
+    reused across calls.  Keyed by (device, stream) and allocated on that
+    stream: launches of one stream are ordered, so they may share it, while
+    partitions running on other streams of the same device (multidevice,
+    a threaded chunk scheduler) each get their own."""
+    t = torch()
+    s = stream if stream is not None else t.cuda.current_stream(device)
+    key = (str(device), int(s.cuda_stream))
     ws = _WORKSPACES.get(key)
     if ws is None or ws.numel() < nbytes:
-        ws = torch().empty(max(nbytes, 1), dtype=torch().uint8, device=device)
+        with t.cuda.stream(s):
+            ws = t.empty(max(nbytes, 1), dtype=t.uint8, device=device)
         _WORKSPACES[key] = ws
     return ws
 
 
-def reserve_affine_workspace(device, ih: int, iw: int) -> None:
-    """Allocate the K2/K3 workspace for an (ih, iw) intermediate up front (a
-    band pipeline must not reallocate it while launches are in flight)."""
-    _workspace(device, _native.lib().xrs_affine_workspace_size(ih, iw))
+def reserve_affine_workspace(device, ih: int, iw: int, stream=None) -> None:
+    """Allocate the K2/K3 workspace of `stream` for an (ih, iw) intermediate
+    up front (a band pipeline must not reallocate it while launches are in
+    flight)."""
+    _workspace(device, _native.lib().xrs_affine_workspace_size(ih, iw), stream)
 
 
 def any_nan(src, stream=None) -> bool:
@@ -507,7 +545,7 @@ def affine(src, plan, out=None, stream=None):
     lib = _native.lib()
     ih, iw = plan.out_h * plan.div_y, plan.out_w * plan.div_x
     nbytes = lib.xrs_affine_workspace_size(ih, iw)
-    ws = _workspace(device, nbytes)
+    ws = _workspace(device, nbytes, stream)
     st, sy, sx = src.stride()
     dt, dy, dx = out.stride()
     if sx != 1 or dx != 1:

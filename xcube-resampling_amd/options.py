@@ -22,6 +22,16 @@
     table traffic overlaps it).  Plans whose tables would exceed this many
     bytes fuse the projection into the gather instead (xrs_reproject_proj: no
     tables, the same values bit for bit).  Default 16 GiB; 0 always fuses.
+
+``devices``:
+    None (default) — every call runs on the current HIP device;
+    a list of devices (ordinals or "cuda:k" strings, repeats allowed) —
+    reproject_dataset / rectify_dataset / affine_transform_dataset (and
+    resample_in_space) split each variable's independent partitions over them
+    from this one process: one host thread and HIP stream per entry, each
+    device holding only the source rows its partition reads
+    (``multidevice``).  The dataset functions also take ``devices=`` as a
+    keyword (it applies to that call and the calls it makes, in its thread).
 """
 
 from __future__ import annotations
@@ -29,10 +39,30 @@ from __future__ import annotations
 import contextlib
 
 _OPTIONS = {"reproject_bilinear_dtype": "float64", "host_streaming_min_bytes": 64 << 20,
-            "reproject_table_max_bytes": 16 << 30}
+            "reproject_table_max_bytes": 16 << 30, "devices": None}
 _ALLOWED = {"reproject_bilinear_dtype": ("float64", "source"),
             "host_streaming_min_bytes": lambda v: isinstance(v, int) and v >= 0,
-            "reproject_table_max_bytes": lambda v: isinstance(v, int) and v >= 0}
+            "reproject_table_max_bytes": lambda v: isinstance(v, int) and v >= 0,
+            "devices": lambda v: v is None or _valid_devices(v)}
+
+
+def _valid_devices(v) -> bool:
+    """A non-empty list / tuple of device ordinals (int >= 0) or "cuda[:k]"
+    strings (torch.device objects of type cuda are accepted too)."""
+    if isinstance(v, (str, bytes)) or not isinstance(v, (list, tuple)) or len(v) == 0:
+        return False
+    for d in v:
+        if isinstance(d, bool):
+            return False
+        if isinstance(d, int):
+            if d < 0:
+                return False
+        elif isinstance(d, str):
+            if not (d == "cuda" or (d.startswith("cuda:") and d[5:].isdigit())):
+                return False
+        elif getattr(d, "type", None) != "cuda":
+            return False
+    return True
 
 
 def get_options() -> dict:

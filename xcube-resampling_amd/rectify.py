@@ -23,7 +23,7 @@ from collections.abc import Iterable
 
 import numpy as np
 
-from . import kernels
+from . import kernels, multidevice
 from .affine import resample_dataset
 from .constants import SCALE_LIMIT, UV_DELTA
 from .crs import Transformer
@@ -49,9 +49,19 @@ def rectify_dataset(source_ds, target_gm: GridMapping | None = None,
                     source_gm: GridMapping | None = None,
                     variables: str | Iterable[str] | None = None, interp_methods=None,
                     agg_methods=None, recover_nans=False, fill_values=None,
-                    tile_size=None) -> Dataset:
+                    tile_size=None, devices=None) -> Dataset:
     """Rectify a dataset with 2-D coordinates onto a regular grid
-    (rectify.py:54-179; same arguments, defaults and errors)."""
+    (rectify.py:54-179; same arguments, defaults and errors).
+    ``devices`` (engine extension): split the target tiles over these GPUs
+    (``multidevice``; default: the ``devices`` option, else the current
+    device)."""
+    with multidevice.use_devices(devices):
+        return _rectify_dataset(source_ds, target_gm, source_gm, variables, interp_methods,
+                                agg_methods, recover_nans, fill_values, tile_size)
+
+
+def _rectify_dataset(source_ds, target_gm, source_gm, variables, interp_methods, agg_methods,
+                     recover_nans, fill_values, tile_size) -> Dataset:
     source_ds = as_dataset(source_ds)
     if source_gm is None:
         source_gm = GridMapping.from_dataset(source_ds)
@@ -73,18 +83,24 @@ def rectify_dataset(source_ds, target_gm: GridMapping | None = None,
     # interpolation (config 4: nearest 1.30 vs 1.41 ms, bilinear 1.42 vs
     # 1.45 ms; with 4 rows the bilinear taps cost a wave per SIMD and fusing
     # it was slower, 1.50 vs 1.47 ms)
-    fused = next((k for k in rect_vars if len(source_ds[k].dims) in (2, 3)
-                  and not _streams(source_ds[k].data)), None)
-    if fused is not None:
-        da = source_ds[fused]
-        src = _var_device(da.data)
-        target_source_ij, out = _compute_target_source_ij(
-            source_gm, target_gm, UV_DELTA, var=(
-                src, _get_interp_method_str(interp_methods, fused, da),
-                _get_fill_value(fill_values, fused, da), len(rect_vars) > 1))
-        fused_da = _rectified_array(da, target_gm, out)
+    devices = multidevice.active_devices()
+    parted, fused = {}, None
+    if devices is not None:   # every variable over the device list (multidevice)
+        parted = _rectify_partitioned(source_ds, source_gm, target_gm, rect_vars,
+                                      interp_methods, fill_values, devices)
     else:
-        target_source_ij = _compute_target_source_ij(source_gm, target_gm, UV_DELTA)
+        fused = next((k for k in rect_vars if len(source_ds[k].dims) in (2, 3)
+                      and not _streams(source_ds[k].data)), None)
+        if fused is not None:
+            da = source_ds[fused]
+            src = _var_device(da.data)
+            target_source_ij, out = _compute_target_source_ij(
+                source_gm, target_gm, UV_DELTA, var=(
+                    src, _get_interp_method_str(interp_methods, fused, da),
+                    _get_fill_value(fill_values, fused, da), len(rect_vars) > 1))
+            fused_da = _rectified_array(da, target_gm, out)
+        else:
+            target_source_ij = _compute_target_source_ij(source_gm, target_gm, UV_DELTA)
 
     x_name, y_name = source_gm.xy_var_names
     coords = {k: v for k, v in source_ds.coords.items() if k not in (x_name, y_name)}
@@ -101,6 +117,9 @@ def rectify_dataset(source_ds, target_gm: GridMapping | None = None,
                 f"Data variable {var_name} has {len(data_array.dims)} dimensions."
             if var_name == fused:
                 target_ds[var_name] = fused_da
+                continue
+            if var_name in parted:
+                target_ds[var_name] = parted[var_name]
                 continue
             target_ds[var_name] = _rectify_data_array(
                 data_array, var_name, target_gm, target_source_ij, interp_methods, fill_values)
@@ -225,6 +244,63 @@ def rectify_tile_run(source_gm: GridMapping, target_gm: GridMapping, src, shard,
     ij = kernels.rectify_ij(xy[0], xy[1], run, ntx, target_gm.height, target_gm.width,
                             target_gm.x_res, dst_y_scale, uv_delta, init_nan=True)
     return kernels.rectify_var(ij, src, interp, fill, rows=shard.rows)
+
+
+def _rectify_partitioned(source_ds, source_gm: GridMapping, target_gm: GridMapping, rect_vars,
+                         interp_methods, fill_values, devices) -> dict:
+    """K5 + K6 over several devices (``multidevice``): the target tiles are
+    dealt as contiguous cost-balanced runs (``sharding.rectify_shard``); each
+    device gets the source coordinates and the variables (a tile's source
+    window can lie anywhere), runs K5 on its tiles and K6 on the target rows
+    they cover, and its tiles' pixels are copied into the variable's output.
+    Tiles are independent (rectify.py:347-370), so the result is the
+    single-device one bit for bit.  Returns {name: DataArray}."""
+    from .sharding import rectify_shard
+
+    dev0 = require_device()
+    xy = source_gm.xy_coords.data
+    xy0 = (host_to_device(xy[0], dev0, np.float64), host_to_device(xy[1], dev0, np.float64))
+    tiles, ntx, _, _ = rectify_tiles(source_gm, target_gm, UV_DELTA, xy=xy0)
+    world = len(devices)
+    shards = [rectify_shard(tiles, world, i) for i in range(world)]
+    dst_y_scale = target_gm.y_res if target_gm.is_j_axis_up else -target_gm.y_res
+
+    def part_ij(i, dev):
+        sh = shards[i]
+        if sh.tile1 <= sh.tile0:
+            return None
+        x, y = (c if c.device == dev else c.to(dev) for c in xy0)
+        return kernels.rectify_ij(x, y, tiles[sh.tile0:sh.tile1], ntx, target_gm.height,
+                                  target_gm.width, target_gm.x_res, dst_y_scale, UV_DELTA,
+                                  init_nan=True)
+
+    ijs = multidevice.run_parts(devices, part_ij, sources=list(xy0))
+    out = {}
+    for name in rect_vars:
+        da = source_ds[name]
+        if len(da.dims) not in (2, 3):
+            continue
+        interp = _get_interp_method_str(interp_methods, name, da)
+        fill = _get_fill_value(fill_values, name, da)
+        data = da.data
+        on_device = is_device_array(data)
+        arr = data if on_device else np.asarray(data)
+        if arr.ndim == 2:
+            arr = arr.unsqueeze(0) if on_device else arr.reshape((1,) + arr.shape)
+        res = multidevice.output_like(arr, (arr.shape[0], target_gm.height, target_gm.width),
+                                      da.dtype)
+
+        def part_var(i, dev, arr=arr, res=res, interp=interp, fill=fill):
+            sh = shards[i]
+            if ijs[i] is None:
+                return
+            src = multidevice.rows_to_device(arr, 0, arr.shape[1], dev)
+            band = kernels.rectify_var(ijs[i], src, interp, fill, rows=sh.rows)
+            multidevice.put_tiles(res, band, tiles[sh.tile0:sh.tile1], sh.row0)
+
+        multidevice.run_parts(devices, part_var, sources=[arr])
+        out[name] = _rectified_array(da, target_gm, res)
+    return out
 
 
 def _compute_target_source_ij(source_gm: GridMapping, target_gm: GridMapping,

@@ -24,7 +24,7 @@ from dataclasses import dataclass, field
 
 import numpy as np
 
-from . import kernels, streaming
+from . import kernels, multidevice, streaming
 from .constants import SCALE_LIMIT
 from .crs import Transformer
 from .dataset import DataArray, Dataset
@@ -73,6 +73,10 @@ class ReprojectPlan:
     # (xrs_reproject_proj) instead of through coordinate tables; also chosen
     # when the tables would exceed the ``reproject_table_max_bytes`` option
     fuse_transform: bool = False
+    # separable plans whose src_x the target grid's column generators
+    # reproduce bit for bit (``column_generators``): K1 computes the column
+    # coordinates instead of reading them (xrs_reproject coord_mode 2)
+    x_gen: np.ndarray | None = None
     _device_cache: dict = field(default_factory=dict, repr=False)
 
     @property
@@ -103,6 +107,8 @@ class ReprojectPlan:
                 sx = to_device(np.ascontiguousarray(self.src_x, np.float64), device)
                 sy = to_device(np.ascontiguousarray(self.src_y, np.float64), device)
             tabs = dict(src_x=sx, src_y=sy, **self._tile_tables(device))
+            if self.x_gen is not None and self.coord_mode == 0:
+                tabs["x_gen"] = to_device(np.ascontiguousarray(self.x_gen, np.float64), device)
             self._device_cache[key] = tabs
         return tabs
 
@@ -275,10 +281,13 @@ def plan_reproject(source_gm: GridMapping, target_gm: GridMapping,
     # target pixel centres in the source CRS (reproject.py:472-496)
     tx = target_gm.x_coords.values
     ty = target_gm.y_coords.values
+    x_gen = None
     if transformer.is_separable:
         coord_mode = 0
         src_x = transformer.transform_x(tx)
         src_y = transformer.transform_y(ty)
+        x_gen = column_generators(tx, target_gm.tile_width, src_x,
+                                  transformer.separable_x_scales())
     else:   # evaluated per target pixel on the device (xrs_transform)
         coord_mode = 1
         src_x = src_y = None
@@ -296,14 +305,59 @@ def plan_reproject(source_gm: GridMapping, target_gm: GridMapping,
         grid_x=None if coord_mode == 0 else np.asarray(tx, np.float64),
         grid_y=None if coord_mode == 0 else np.asarray(ty, np.float64),
         transformer=None if coord_mode == 0 else transformer,
+        x_gen=x_gen,
     )
+
+
+def column_generators(tx, tile_w: int, src_x, scales) -> np.ndarray | None:
+    """xrs_reproject's coord_mode-2 records (include/xrs.h) for a separable
+    plan, or None when they would not reproduce ``src_x`` bit for bit.
+
+    A regular target grid's x coordinates are dask's blockwise linspace of
+    the pixel centres, one block per tile column (regular.py:44-52 ->
+    ``helpers.dask_linspace``): element k of a block of n is k * step + start,
+    the last one stop.  The separable transformation then scales them
+    (``Transformer.separable_x_scales``).  K1 can evaluate that itself from
+    32 bytes per tile column instead of reading 8 bytes per column — but only
+    the comparison below, on every column, licenses it."""
+    if scales is None or tile_w < 1:
+        return None
+    tx = np.asarray(tx, np.float64)
+    w = tx.size
+    m1, m2 = (float(v) for v in scales)
+    gen = np.empty(w, np.float64)
+    recs = []
+    for b0 in range(0, w, tile_w):
+        n = min(tile_w, w - b0)
+        start, stop = float(tx[b0]), float(tx[b0 + n - 1])
+        step = (stop - start) / (n - 1) if n > 1 else 0.0
+        v = np.arange(n, dtype=np.float64) * step + start
+        v[-1] = stop
+        gen[b0:b0 + n] = v
+        recs.append((start, stop, step, float(n)))
+    with np.errstate(all="ignore"):
+        x = (gen * m1) * m2
+    if not np.array_equal(x.view(np.uint64), np.ascontiguousarray(src_x, np.float64).view(np.uint64)):
+        return None
+    return np.concatenate([np.asarray(recs, np.float64).reshape(-1), [m1, m2]])
 
 
 def reproject_dataset(source_ds, target_gm: GridMapping, source_gm: GridMapping | None = None,
                       variables: str | Iterable[str] | None = None, interp_methods=None,
-                      agg_methods=None, recover_nans=False, fill_values=None) -> Dataset:
+                      agg_methods=None, recover_nans=False, fill_values=None,
+                      devices=None) -> Dataset:
     """Reproject a dataset to the CRS and grid of ``target_gm``
-    (reproject.py:51-186; same arguments, defaults and errors)."""
+    (reproject.py:51-186; same arguments, defaults and errors).
+    ``devices`` (engine extension): split every variable's target row bands
+    over these GPUs (``multidevice``; default: the ``devices`` option, else
+    the current device)."""
+    with multidevice.use_devices(devices):
+        return _reproject_dataset(source_ds, target_gm, source_gm, variables, interp_methods,
+                                  agg_methods, recover_nans, fill_values)
+
+
+def _reproject_dataset(source_ds, target_gm, source_gm, variables, interp_methods, agg_methods,
+                       recover_nans, fill_values) -> Dataset:
     source_ds = as_dataset(source_ds)
     if source_gm is None:
         source_gm = GridMapping.from_dataset(source_ds)
@@ -361,7 +415,14 @@ def _reproject_data_array(data_array: DataArray, var_name, target_gm: GridMappin
     if interp_method == "bilinear" and get_options()["reproject_bilinear_dtype"] == "source":
         out_dtype = data_array.dtype if np.issubdtype(data_array.dtype, np.floating) else np.float64
     expanded = len(data_array.dims) == 2
-    if not on_device and isinstance(data, np.ndarray) and \
+    devices = multidevice.active_devices()
+    if devices is not None:
+        # the variable's target row bands over several devices (multidevice)
+        src = data if on_device else np.asarray(data)
+        src = src.unsqueeze(0) if (expanded and on_device) else \
+            (src.reshape((1,) + src.shape) if expanded else src)
+        result = _reproject_partitioned(src, plan, interp_method, fill_value, out_dtype, devices)
+    elif not on_device and isinstance(data, np.ndarray) and \
             data.nbytes >= get_options()["host_streaming_min_bytes"]:
         # host array in, host array out (reproject.py:254-255): band pipeline
         src = data.reshape((1,) + data.shape) if expanded else data
@@ -379,6 +440,44 @@ def _reproject_data_array(data_array: DataArray, var_name, target_gm: GridMappin
     else:
         dims = (data_array.dims[0], target_gm.xy_dim_names[1], target_gm.xy_dim_names[0])
     return DataArray(result, dims, data_array.attrs)
+
+
+def _reproject_partitioned(src, plan: ReprojectPlan, interp: str, fill, out_dtype, devices):
+    """K1 over several devices (``multidevice``): target row bands balanced by
+    predicted K1 time (``sharding.band_shard``; by rows for 2-D plans), each
+    device holding only the source rows its band reads, from one host thread
+    and stream per device.  The band results land in one (n, H', W') output —
+    numpy for a numpy source, a tensor on the source's device otherwise — bit
+    for bit the single-launch result (the kernel takes any row band:
+    reproject.py:230-252's per-tile blocks are independent)."""
+    from .sharding import band_shard
+
+    od = np.dtype(out_dtype if out_dtype is not None else
+                  (np.float64 if interp == "bilinear" else _src_dtype(src)))
+    world = len(devices)
+    balance = "cost" if plan.coord_mode == 0 else "rows"
+    shards = [band_shard(plan, world, i, balance, od.itemsize) for i in range(world)]
+    n = src.shape[0]
+    out = multidevice.output_like(src, (n, plan.dst_height, plan.dst_width), od)
+
+    def part(i, dev):
+        sh = shards[i]
+        if sh.row1 <= sh.row0:
+            return
+        j0, j1 = sh.src_rows
+        band = multidevice.rows_to_device(src, j0, j1, dev)
+        res = kernels.reproject(band, plan, interp, fill, out_dtype=od, rows=sh.rows, src_row0=j0)
+        multidevice.put_rows(out, sh.row0, sh.row1, res)
+
+    multidevice.run_parts(devices, part, sources=[src])
+    return out
+
+
+def _src_dtype(src) -> np.dtype:
+    if is_device_array(src):
+        from .device import numpy_dtype
+        return numpy_dtype(src.dtype)
+    return np.dtype(src.dtype)
 
 
 def _downscale_source_dataset(source_ds, source_gm: GridMapping, target_gm: GridMapping,

@@ -4,6 +4,7 @@ from __future__ import annotations
 
 from collections.abc import Iterable
 
+from . import multidevice
 from .affine import affine_transform_dataset
 from .constants import LOG
 from .gridmapping import GridMapping
@@ -15,9 +16,19 @@ from .utils import _can_apply_affine_transform, as_dataset
 def resample_in_space(source_ds, target_gm: GridMapping | None = None,
                       source_gm: GridMapping | None = None,
                       variables: str | Iterable[str] | None = None, interp_methods=None,
-                      agg_methods=None, recover_nans=False, fill_values=None, tile_size=None):
+                      agg_methods=None, recover_nans=False, fill_values=None, tile_size=None,
+                      devices=None):
     """Irregular source -> rectify; regular + same CRS (or both geographic) ->
-    affine; otherwise -> reproject; close grid mappings -> the input."""
+    affine; otherwise -> reproject; close grid mappings -> the input.
+    ``devices`` (engine extension): the GPUs each variable's partitions are
+    spread over (``multidevice``)."""
+    with multidevice.use_devices(devices):
+        return _resample_in_space(source_ds, target_gm, source_gm, variables, interp_methods,
+                                  agg_methods, recover_nans, fill_values, tile_size)
+
+
+def _resample_in_space(source_ds, target_gm, source_gm, variables, interp_methods, agg_methods,
+                       recover_nans, fill_values, tile_size):
     source_ds = as_dataset(source_ds)
     if source_gm is None:
         source_gm = GridMapping.from_dataset(source_ds)

@@ -20,6 +20,7 @@ to the resident path: the same K1 launch, restricted to the band's rows.
 
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import threading
 
@@ -132,20 +133,51 @@ class _Staging:
                 self.events[i] = None
 
 
-_STAGING = threading.local()
+_POOL_MAX = 8                # staging pairs a process keeps at most (8 x 32 MiB page-locked)
+_POOL_COND = threading.Condition()
+_POOL_FREE: list = []
+_POOL_MADE = 0
 
 
-def _staging() -> _Staging:
-    """This thread's staging buffers.  A _Staging holds shared state (the
-    buffer index, the events of the DMAs still using each buffer) that two
-    threads must not interleave — a threaded chunk scheduler calling the
-    dataset APIs from several threads would overwrite each other's staged
-    bytes — so every thread that streams gets its own pair (allocated on its
-    first streamed copy, 2 x 16 MiB page-locked)."""
-    st = getattr(_STAGING, "st", None)
+@contextlib.contextmanager
+def _staging():
+    """A pair of staging buffers, borrowed for one streamed transfer.  A
+    _Staging holds state (the buffer index, the events of the DMAs still using
+    each buffer) that two threads must not interleave, so a thread takes a
+    pair from a small process-wide pool and returns it drained; at most
+    _POOL_MAX pairs are ever allocated (a threaded chunk scheduler with many
+    workers waits for a free pair instead of pinning 32 MiB per thread,
+    ADVICE r04)."""
+    global _POOL_MADE
+    with _POOL_COND:
+        while not _POOL_FREE and _POOL_MADE >= _POOL_MAX:
+            _POOL_COND.wait()
+        if _POOL_FREE:
+            st = _POOL_FREE.pop()
+        else:
+            _POOL_MADE += 1
+            st = None
     if st is None:
-        st = _STAGING.st = _Staging()
-    return st
+        try:
+            st = _Staging()
+        except BaseException:
+            with _POOL_COND:
+                _POOL_MADE -= 1
+                _POOL_COND.notify()
+            raise
+    try:
+        yield st
+    finally:
+        try:
+            st.drain()
+        finally:
+            with _POOL_COND:
+                _POOL_FREE.append(st)
+                _POOL_COND.notify()
+
+
+def _small(nbytes: int) -> bool:
+    return nbytes < max(1, get_options()["host_streaming_min_bytes"])
 
 
 def host_to_device(arr, device, dtype=None):
@@ -155,33 +187,61 @@ def host_to_device(arr, device, dtype=None):
     if not isinstance(arr, np.ndarray):
         return to_device(arr, device, dtype)
     arr = np.ascontiguousarray(arr if dtype is None else arr.astype(dtype, copy=False))
-    if arr.nbytes < max(1, get_options()["host_streaming_min_bytes"]) or \
-            arr.dtype not in _native.DTYPE_CODES:
+    if _small(arr.nbytes) or arr.dtype not in _native.DTYPE_CODES:
         return to_device(arr, device)
     dst = empty(arr.shape, arr.dtype, device)
+    with _staging() as st:
+        st.h2d(dst.data_ptr(), arr, torch().cuda.current_stream(device))
+    return dst
+
+
+def host_rows_to_device(arr: np.ndarray, j0: int, j1: int, device):
+    """Rows [j0, j1) of every slice of a host (n, H, W) array as a contiguous
+    device tensor (n, j1 - j0, W), slice by slice through the staging buffers
+    (no host copy of the strided band first)."""
+    n, _, w = arr.shape
+    rows = max(0, j1 - j0)
+    dst = empty((n, rows, w), arr.dtype, device)
+    if rows == 0:
+        return dst
+    if _small(n * rows * w * arr.itemsize) or arr.dtype not in _native.DTYPE_CODES:
+        dst.copy_(torch().from_numpy(np.ascontiguousarray(arr[:, j0:j1])))
+        return dst
     stream = torch().cuda.current_stream(device)
-    st = _staging()
-    try:
-        st.h2d(dst.data_ptr(), arr, stream)
-    finally:
-        st.drain()
+    with _staging() as st:
+        for s in range(n):
+            st.h2d(dst[s].data_ptr(), arr[s, j0:j1], stream)
     return dst
 
 
 def device_to_host(x) -> np.ndarray:
     """device tensor -> numpy through the page-locked staging buffers, for
     tensors of at least ``host_streaming_min_bytes``."""
-    nbytes = x.numel() * x.element_size()
-    if nbytes < max(1, get_options()["host_streaming_min_bytes"]):
+    if _small(x.numel() * x.element_size()):
         return x.cpu().numpy()
-    x = x.contiguous()
     out = np.empty(tuple(x.shape), numpy_dtype(x.dtype))
-    st = _staging()
-    try:
-        st.d2h(out, x.data_ptr(), torch().cuda.current_stream(x.device))
-    finally:
-        st.drain()
+    device_to_host_into(out, x)
     return out
+
+
+def device_to_host_into(out: np.ndarray, x) -> None:
+    """out[...] = x (device tensor of out's shape), slice by slice through the
+    staging buffers; `out` may be a strided view of a C-contiguous array whose
+    last two axes are contiguous per slice (a row band of a result)."""
+    if _small(x.numel() * x.element_size()) or out.ndim != 3:
+        out[...] = x.cpu().numpy()
+        return
+    x = x.contiguous()
+    stream = torch().cuda.current_stream(x.device)
+    with _staging() as st:
+        for s in range(out.shape[0]):
+            dst = out[s]
+            if dst.flags.c_contiguous:
+                st.d2h(dst, x[s].data_ptr(), stream)
+            else:
+                tmp = np.empty(dst.shape, dst.dtype)
+                st.d2h(tmp, x[s].data_ptr(), stream)
+                dst[...] = tmp
 
 
 def band_ranges(height: int, band_rows: int) -> list[tuple[int, int]]:
@@ -249,35 +309,35 @@ def reproject_host(src: np.ndarray, plan, interp: str, fill: float, out_dtype=No
         plan.device_tables(device)
     for s in (s_in, s_k, s_out):
         s.wait_stream(cur)
-    st = _staging()
-    prev = None   # the band whose copy-out is pending: it overlaps the next kernel
-    try:
-        hi = 0
-        for b, ((r0, r1), (_, j1)) in enumerate(zip(bands, src_rows)):
-            if j1 > hi:   # rows [hi, j1) of every slice (contiguous per slice)
-                for s in range(n):
-                    st.h2d(dsrc[s, hi].data_ptr(), src[s, hi:j1], s_in)
-                hi = j1
-            ev_in = t.cuda.Event()
-            ev_in.record(s_in)
-            s_k.wait_event(ev_in)
-            # bufs[b % 2] held band b - 2, whose copy-out has landed (d2h returns
-            # when the bytes are in `out`)
-            buf = bufs[b % 2][:, :r1 - r0]
-            kernels.reproject(dsrc, plan, interp, fill, out_dtype=out_dtype, rows=(r0, r1),
-                              out=buf, flags=flags, stream=s_k)
-            ev_k = t.cuda.Event()
-            ev_k.record(s_k)
+    with _staging() as st:
+        prev = None   # the band whose copy-out is pending: it overlaps the next kernel
+        try:
+            hi = 0
+            for b, ((r0, r1), (_, j1)) in enumerate(zip(bands, src_rows)):
+                if j1 > hi:   # rows [hi, j1) of every slice (contiguous per slice)
+                    for s in range(n):
+                        st.h2d(dsrc[s, hi].data_ptr(), src[s, hi:j1], s_in)
+                    hi = j1
+                ev_in = t.cuda.Event()
+                ev_in.record(s_in)
+                s_k.wait_event(ev_in)
+                # bufs[b % 2] held band b - 2, whose copy-out has landed (d2h returns
+                # when the bytes are in `out`)
+                buf = bufs[b % 2][:, :r1 - r0]
+                kernels.reproject(dsrc, plan, interp, fill, out_dtype=out_dtype, rows=(r0, r1),
+                                  out=buf, flags=flags, stream=s_k)
+                ev_k = t.cuda.Event()
+                ev_k.record(s_k)
+                if prev is not None:
+                    _copy_out(st, out, prev, s_out)
+                prev = (r0, r1, buf, ev_k)
             if prev is not None:
                 _copy_out(st, out, prev, s_out)
-            prev = (r0, r1, buf, ev_k)
-        if prev is not None:
-            _copy_out(st, out, prev, s_out)
-    finally:   # nothing may still use the device buffers when they are freed
-        st.drain()
-        s_in.synchronize()
-        s_k.synchronize()
-        s_out.synchronize()
+        finally:   # nothing may still use the device buffers when they are freed
+            st.drain()
+            s_in.synchronize()
+            s_k.synchronize()
+            s_out.synchronize()
     flags.raise_if_set("reproject")
     return out
 
@@ -337,29 +397,29 @@ def band_pipeline(src: np.ndarray, dsrc, out: np.ndarray, bands, src_rows, launc
     s_in, s_k, s_out = (t.cuda.Stream(device) for _ in range(3))
     for s in (s_in, s_k, s_out):
         s.wait_stream(cur)
-    st = _staging()
-    rows = _SourceRows(src, dsrc, s_in, st)
-    prev = None   # the band whose copy-out is pending: it overlaps the next kernel
-    try:
-        for b, ((r0, r1), (j0, j1)) in enumerate(zip(bands, src_rows)):
-            rows.need(j0, j1)
-            ev_in = t.cuda.Event()
-            ev_in.record(s_in)
-            s_k.wait_event(ev_in)
-            buf = bufs[b % 2][:, :r1 - r0]   # band b - 2's copy-out has landed
-            launch(b, r0, r1, buf, s_k)
-            ev_k = t.cuda.Event()
-            ev_k.record(s_k)
+    with _staging() as st:
+        rows = _SourceRows(src, dsrc, s_in, st)
+        prev = None   # the band whose copy-out is pending: it overlaps the next kernel
+        try:
+            for b, ((r0, r1), (j0, j1)) in enumerate(zip(bands, src_rows)):
+                rows.need(j0, j1)
+                ev_in = t.cuda.Event()
+                ev_in.record(s_in)
+                s_k.wait_event(ev_in)
+                buf = bufs[b % 2][:, :r1 - r0]   # band b - 2's copy-out has landed
+                launch(b, r0, r1, buf, s_k)
+                ev_k = t.cuda.Event()
+                ev_k.record(s_k)
+                if prev is not None:
+                    _copy_out(st, out, prev, s_out)
+                prev = (r0, r1, buf, ev_k)
             if prev is not None:
                 _copy_out(st, out, prev, s_out)
-            prev = (r0, r1, buf, ev_k)
-        if prev is not None:
-            _copy_out(st, out, prev, s_out)
-    finally:   # nothing may still use the device buffers when they are freed
-        st.drain()
-        s_in.synchronize()
-        s_k.synchronize()
-        s_out.synchronize()
+        finally:   # nothing may still use the device buffers when they are freed
+            st.drain()
+            s_in.synchronize()
+            s_k.synchronize()
+            s_out.synchronize()
     return out
 
 
@@ -449,11 +509,12 @@ def affine_host(src: np.ndarray, plan, device=None, band_chunks: int | None = No
                                          _cache={}))
     for p in plans:   # small tables, uploaded before the streams start
         p.device_tables(device)
-    kernels.reserve_affine_workspace(device, max(p.out_h for p in plans) * plan.div_y,
-                                     plan.out_w * plan.div_x)
     dsrc = empty((nt, h, w), src.dtype, device)
 
     def launch(b, r0, r1, buf, stream):
+        if b == 0:   # the kernel stream's workspace, sized for the tallest band
+            kernels.reserve_affine_workspace(device, max(p.out_h for p in plans) * plan.div_y,
+                                             plan.out_w * plan.div_x, stream)
         kernels.affine(dsrc, plans[b], out=buf, stream=stream)
 
     return band_pipeline(src, dsrc, out, bands, src_rows, launch, device, poison)
