@@ -109,6 +109,82 @@ def _cpu_pool(fn, seconds):
     return px / dt / 1e6, px, dt, cores
 
 
+# the issue-bound rectify kernels: one rocprofv3 --pmc pass (6 SQ + 2 GRBM
+# counters) of scripts/time_rectify.py --fused, reduced per kernel
+ISSUE_COUNTERS = ["SQ_ACTIVE_INST_VALU", "SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_WAVE_CYCLES",
+                  "SQ_WAIT_ANY", "SQ_ACTIVE_INST_ANY", "GRBM_GUI_ACTIVE", "GRBM_COUNT"]
+N_SIMD = 1024   # 256 CUs x 4 SIMDs
+N_XCD = 8
+
+
+def issue_pmc(kernels=("claim", "resolve", "ij_bboxes"), timeout=150):
+    """Per kernel: VALU-issue fraction = 4 x SQ_ACTIVE_INST_VALU (quad-cycles
+    of VALU issue, summed over the SIMDs) / (N_SIMD x GRBM_GUI_ACTIVE / N_XCD
+    (the dispatch's shader cycles; the GRBM counter sums the 8 XCDs)): the
+    share of the SIMDs' cycles spent issuing vector instructions at the
+    nominal 4 cycles per wave64 instruction — the roof of an issue-bound
+    kernel, as the HBM fraction is of a memory-bound one.  Also the wave
+    cycles parked on memory (SQ_WAIT_ANY / SQ_WAVE_CYCLES).  Runs as a child
+    process while this one is idle; None when rocprofv3 is absent or fails."""
+    import csv
+    import shutil
+    import subprocess
+    import tempfile
+    from collections import defaultdict
+
+    prof = shutil.which("rocprofv3")
+    if prof is None:
+        return None
+    d = tempfile.mkdtemp(prefix="xrs_issue_", dir=os.environ.get("TMPDIR", "/tmp"))
+    try:
+        cmd = ["timeout", "-s", "KILL", str(timeout), prof, "--pmc", *ISSUE_COUNTERS,
+               "--kernel-trace", "--output-format", "csv", "-d", d, "-o", "p", "--",
+               sys.executable, os.path.join(ROOT, "scripts", "time_rectify.py"), "--fused",
+               "--reps", "3"]
+        r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+        if r.returncode != 0:
+            print(f"issue_pmc: rocprofv3 failed (rc {r.returncode}):\n{r.stdout[-1500:]}",
+                  file=sys.stderr)
+            return None
+        acc = defaultdict(float)
+        disp = defaultdict(set)
+        for path in _find(d, "counter_collection.csv"):
+            for row in csv.DictReader(open(path)):
+                k = next((n for n in kernels if n in row["Kernel_Name"]), None)
+                if k is None:
+                    continue
+                acc[(k, row["Counter_Name"])] += float(row["Counter_Value"])
+                disp[k].add(row["Dispatch_Id"])
+        out = {}
+        for k in kernels:
+            n = len(disp[k])
+            if not n:
+                continue
+            c = {name: acc[(k, name)] / n for name in ISSUE_COUNTERS}
+            cyc = c["GRBM_GUI_ACTIVE"] / N_XCD
+            out[k] = {"valu_issue_frac": round(4 * c["SQ_ACTIVE_INST_VALU"] / (N_SIMD * cyc), 4)
+                      if cyc else None,
+                      "valu_wave_insts": int(c["SQ_INSTS_VALU"]),
+                      "salu_wave_insts": int(c["SQ_INSTS_SALU"]),
+                      "wait_frac": round(c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"], 4)
+                      if c["SQ_WAVE_CYCLES"] else None,
+                      "shader_cycles": int(cyc), "dispatches": n}
+        out["method"] = ("rocprofv3 --pmc " + " ".join(ISSUE_COUNTERS) + " on scripts/"
+                         "time_rectify.py --fused (the config-4 pass): valu_issue_frac = 4 x "
+                         "SQ_ACTIVE_INST_VALU / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs); "
+                         "wait_frac = SQ_WAIT_ANY / SQ_WAVE_CYCLES")
+        return out
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+
+
+def _find(root, suffix):
+    for dp, _, files in os.walk(root):
+        for f in files:
+            if f.endswith(suffix):
+                yield os.path.join(dp, f)
+
+
 # ------------------------------------------------------------------ config 1
 def config1(args):
     """Affine nearest 1024^2 f32, EPSG:4326 -> EPSG:4326 (scale 0.9216)."""
@@ -405,9 +481,13 @@ def config4(args):
 
     npx = tgm.width * tgm.height
     S = w * h
+    torch.cuda.synchronize()
+    issue = issue_pmc()   # the claim is VALU-issue bound, the resolve waits on memory
     for interp in ("nearest", "bilinear"):
-        ms, wall = _timed(lambda: pipeline(interp), max(3, args.steps // 4), 1)
-        sep_ms, _ = _timed(lambda: separate(interp), max(3, args.steps // 4), 1)
+        # 20 steps after 5 warm-up passes (5 after 1 let the shader clock's
+        # ramp into the timed steps: 0.97 vs 0.90 ms for the same kernels)
+        ms, wall = _timed(lambda: pipeline(interp), args.steps, max(5, args.warmup))
+        sep_ms, _ = _timed(lambda: separate(interp), args.steps, max(5, args.warmup))
         cores = len(os.sched_getaffinity(0))
         # CPU baseline on the config itself: the C restatement of the numba
         # kernels (K4 bboxes + K5 + K6, tiles on a thread pool of all cores)
@@ -433,7 +513,8 @@ def config4(args):
                           f"C restatement of the numba kernels (bboxes, ij, var image; tiles "
                           f"on a {cores}-thread pool), best of 3 passes: {dt:.2f} s"),
               {"covered_px": covered, "k5_ms": round(k5_ms, 4),
-               "k6_ms": round(lines[interp], 4), "unfused_ms": round(sep_ms, 4)})
+               "k6_ms": round(lines[interp], 4), "unfused_ms": round(sep_ms, 4),
+               "issue": issue})
     flags.raise_if_set("config 4")
 
 

@@ -1,6 +1,6 @@
 """K1 work-shape arms through the test-only knobs (band height, grid cap in
-blocks per CU = a persistent grid walking the band-major list in lockstep,
-column groups), timed interleaved on one box against the product shape;
+blocks per CU = a persistent grid walking the band-major list in lockstep),
+timed interleaved on one box against the product shape;
 every arm's raster is compared with the product's bit for bit.
     python scripts/k1_knob_ab.py [--passes 2] [--steps 20] [--arms NAME,...]"""
 from __future__ import annotations
@@ -15,9 +15,10 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-# (name, band rows, blocks per CU (0 = one-shot items), column group (0 = bands))
-ARMS = [("base", 0, 0, 0), ("b8p4", 8, 4, 0), ("b8p2", 8, 2, 0), ("b16p4", 16, 4, 0),
-        ("b32p4", 32, 4, 0), ("b4p4", 4, 4, 0), ("b8", 8, 0, 0), ("b16", 16, 0, 0)]
+# (name, band rows, blocks per CU (0 = one-shot items))
+ARMS = [("base", 0, 0), ("b8p4", 8, 4), ("b8p2", 8, 2), ("b16p4", 16, 4), ("b32p4", 32, 4),
+        ("b4p4", 4, 4), ("b8", 8, 0), ("b16", 16, 0), ("b24", 24, 0), ("b40", 40, 0),
+        ("b48", 48, 0), ("b64", 64, 0)]
 
 
 def main():
@@ -42,8 +43,8 @@ def main():
     lib = bench.load_benchlib()
     stream = torch.cuda.current_stream(dev)
     for p in range(args.passes):
-        for name, band, bpc, group in arms:
-            with testing_knob("reproject_band", band), testing_knob("reproject_xcd_group", group), \
+        for name, band, bpc in arms:
+            with testing_knob("reproject_band", band), \
                     testing_knob("reproject_blocks_per_cu", bpc):
                 step = lambda: kernels.reproject(src, plan, "bilinear", float("nan"),  # noqa
                                                  out_dtype=np.float32, out=out, flags=flags,
@@ -65,7 +66,6 @@ def main():
                 same = bool(torch.equal(out.view(torch.int32), ref.view(torch.int32)))
             flags.raise_if_set("k1 arm")
             print(json.dumps({"arm": name, "band": band or 32, "blocks_per_cu": bpc,
-                              "column_group": group,
                               "pass": p + 1, "ms_per_launch": round(ms, 4),
                               "bit_equal_to_base": same}), flush=True)
 

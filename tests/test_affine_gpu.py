@@ -297,3 +297,38 @@ def test_config3_full_size_sampled_blocks():
         got = out[:, r0 // k:(r0 + c) // k, c0 // k:(c0 + c) // k].cpu().numpy()
         assert np.isnan(a).any(), "the sample must exercise the NaN path"
         assert_bitwise_equal(got, np.asarray(ref)[:, :c // k, :c // k], f"block at ({r0}, {c0})")
+
+
+@pytest.mark.parametrize("nt,interp,dtype", [(7, 0, np.float32), (64, 0, np.float32),
+                                             (5, 0, np.uint8), (1, 1, np.float32),
+                                             (1, 1, np.int16), (3, 0, np.float64),
+                                             (1, 0, np.float32)])
+def test_k2_slice_groups_match_oracle(nt, interp, dtype):
+    """K2's grouped items (slices sharing one geometry: order 0, or order 1
+    without a time neighbour; S slices per item, the last group short) ==
+    the oracle slice by slice — the dask shape of config 1 (many chunks of
+    one grid stacked on dim 0)."""
+    import torch
+
+    import xcube_resampling_amd.affine as A
+    from oracle import affine_ref
+
+    rng = np.random.default_rng(40 + nt)
+    n = 96
+    a = (rng.random((nt, n, n)) * 200).astype(dtype)
+    if np.issubdtype(dtype, np.floating):
+        a.ravel()[rng.random(a.size) < 0.01] = np.nan
+    m = ((0.9216, 0.0, 7.4), (0.0, 0.9216, 5.0))
+    fill = np.nan if np.issubdtype(dtype, np.floating) else 7
+    src = a if nt > 1 else a[0]
+    oshape = ((nt,) if nt > 1 else ()) + (n, n)
+    ochunks = ((1,) if nt > 1 else ()) + (40, 48)
+    plan = A.plan_affine((nt, n, n), np.dtype(dtype), m, oshape, ochunks, interp, "first",
+                         False, fill)
+    assert plan.agg_code == 0 and (interp == 0 or plan.t_next is None)
+    got = A._resample_array(src, None, None, m, oshape, ochunks, interp, "first", False, fill)
+    got = got.cpu().numpy() if isinstance(got, torch.Tensor) else got
+    for t in range(nt):
+        ref = affine_ref.resample_array(a[t:t + 1], m, (1, n, n), (1, 40, 48), interp, "first",
+                                        False, fill)
+        assert_bitwise_equal(got[t] if nt > 1 else got, np.asarray(ref)[0], f"slice {t}")

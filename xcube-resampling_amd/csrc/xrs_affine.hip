@@ -326,6 +326,8 @@ __device__ inline int32_t wave_uniform(int32_t v) { return __builtin_amdgcn_read
 // before the first is used, so a thread pays the entry -> tap -> store chain
 // once for kDirectRows pixels (config 1: one resident round of blocks).
 constexpr int kDirectRows = 4;
+constexpr int kDirectSlices0 = 4;   // slices per grouped K2 item, order 0 (taps in flight: 16)
+constexpr int kDirectSlices1 = 2;   // order 1 (4 taps per pixel: 32)
 
 template <typename T, typename I, int ORDER, bool RECOVER, bool HAS_T1>
 __device__ inline void direct_rows(const AffineArgs& a, const AxisChunks& ay, const Src<T>& p,
@@ -344,6 +346,86 @@ __device__ inline void direct_rows(const AffineArgs& a, const AxisChunks& ay, co
     if (oj0 + q >= a.out_h) break;
     const I v = tp[q].template eval<I, ORDER, RECOVER, HAS_T1>(ey[q], ex, a.cval);
     store_value<I>(a, t * a.dst_st + (oj0 + q) * a.dst_sy + oi, v);
+  }
+}
+
+// The output dtype code of an intermediate type (K2's output dtype is its
+// intermediate dtype for every plan the host makes: plain affine and the
+// first / last / center picks keep it; anything else takes store_any).
+template <typename I> constexpr int dtype_code() {
+  return std::is_same<I, float>::value ? XRS_DTYPE_F32 : std::is_same<I, double>::value ? XRS_DTYPE_F64
+       : std::is_same<I, uint8_t>::value ? XRS_DTYPE_U8 : std::is_same<I, int8_t>::value ? XRS_DTYPE_I8
+       : std::is_same<I, uint16_t>::value ? XRS_DTYPE_U16 : std::is_same<I, int16_t>::value ? XRS_DTYPE_I16
+       : std::is_same<I, uint32_t>::value ? XRS_DTYPE_U32 : std::is_same<I, int32_t>::value ? XRS_DTYPE_I32
+       : std::is_same<I, int64_t>::value ? XRS_DTYPE_I64 : 0;
+}
+
+template <typename I>
+__device__ inline void store_typed(const AffineArgs& a, int64_t didx, I v) {
+  if (a.dst_dtype == dtype_code<I>()) {   // wave-uniform
+    I* d = static_cast<I*>(a.dst) + didx;
+    if (std::is_floating_point<I>::value) __builtin_nontemporal_store(v, d);
+    else *d = v;
+  } else {
+    store_value<I>(a, didx, v);
+  }
+}
+
+// K2 for slices that share one geometry — order 0, or order 1 without a
+// zero-weight time neighbour (the dask shape: many chunks of one grid stacked
+// on dim 0).  A work item is S consecutive slices x kItemH output rows x 64
+// columns: the column entry and the kDirectRows row entries of a wave are
+// evaluated once for all S slices, and the taps of S x kDirectRows pixels
+// are in flight together per lane.  Items are listed band by band (a band =
+// every 64-column tile of one slice group's kItemH rows) and the XCDs take
+// whole bands in turn (K1 / K3i's deal: the items in flight cover one
+// contiguous run of source rows; xcd_slice's eight contiguous eighths were
+// slower for both).  Stores are typed (no per-pixel dtype switch).
+template <typename T, typename I, int ORDER, bool RECOVER, int S>
+__global__ void __launch_bounds__(kThreads)
+affine_direct_group_kernel(AffineArgs a, AxisChunks ay, AxisChunks ax) {
+  constexpr int64_t kItemH = kTileH * kDirectRows;
+  const int tx = threadIdx.x % kTileW;
+  const int ty = wave_uniform(threadIdx.x / kTileW);
+  const int64_t ntx = (a.out_w + kTileW - 1) / kTileW, nty = (a.out_h + kItemH - 1) / kItemH;
+  const int64_t ngroups = (a.nt + S - 1) / S;
+  const int64_t nwork = ntx * nty * ngroups;
+  int sj = 0, si = 0;
+  if (a.agg == AGG_LAST) { sj = (int)a.dy - 1; si = (int)a.dx - 1; }
+  if (a.agg == AGG_CENTER) { sj = (int)a.dy / 2; si = (int)a.dx / 2; }
+  for (XcdGroups sg = xcd_groups(nwork, ntx);; sg.i += sg.step) {
+    const int64_t w = sg.item();
+    if (w >= nwork) break;
+    const int64_t band = w / ntx, ti = w - band * ntx;
+    const int64_t grp = band / nty, tj = band - grp * nty;
+    const int64_t oj0 = tj * kItemH + ty * kDirectRows, oi = ti * kTileW + tx;
+    if (oj0 >= a.out_h || oi >= a.out_w) continue;
+    const AxisTab ex = axis_entry<ORDER>(ax, oi * a.dx + si);
+    AxisTab ey[kDirectRows];
+#pragma unroll
+    for (int q = 0; q < kDirectRows; ++q)
+      ey[q] = oj0 + q < a.out_h ? axis_entry<ORDER>(ay, (oj0 + q) * a.dy + sj)
+                                : AxisTab{-1, -1, 0.0, 0.0};   // wave-uniform
+    const int64_t t0 = grp * S;
+    Taps<T> tp[S][kDirectRows];
+#pragma unroll
+    for (int k = 0; k < S; ++k) {
+      Src<T> p;   // a slice past nt (the last group) reads slice t0: a valid address
+      p.g0 = p.g1 = static_cast<const T*>(a.src) + (t0 + k < a.nt ? t0 + k : t0) * a.src_st;
+      p.sy = a.src_sy;
+#pragma unroll
+      for (int q = 0; q < kDirectRows; ++q) tp[k][q].template load<ORDER, false>(p, ey[q], ex);
+    }
+#pragma unroll
+    for (int k = 0; k < S; ++k) {
+      if (t0 + k >= a.nt) break;
+#pragma unroll
+      for (int q = 0; q < kDirectRows; ++q) {
+        if (oj0 + q >= a.out_h) break;
+        const I v = tp[k][q].template eval<I, ORDER, RECOVER, false>(ey[q], ex, a.cval);
+        store_typed<I>(a, (t0 + k) * a.dst_st + (oj0 + q) * a.dst_sy + oi, v);
+      }
+    }
   }
 }
 
@@ -902,11 +984,25 @@ int launch(const AffineArgs& a, const AxisChunks& ay, const AxisChunks& ax, Axis
   args.ytab = ytab;
   args.xtab = xtab;
   if (direct) {   // one launch: the kernel evaluates its two table entries inline
-    const int64_t ntiles = ((a.out_w + kTileW - 1) / kTileW) *
-                           ((a.out_h + kTileH * kDirectRows - 1) / (kTileH * kDirectRows)) * a.nt;
-    const int nb = grid_blocks(ntiles, 1, 256 * 64);
-    hipLaunchKernelGGL((affine_direct_kernel<T, I, ORDER, RECOVER>), dim3(nb), dim3(kThreads), 0,
-                       st, args, ay, ax);
+    const int64_t bands = (a.out_h + kTileH * kDirectRows - 1) / (kTileH * kDirectRows);
+    const int64_t ntx = (a.out_w + kTileW - 1) / kTileW;
+    if (ORDER == 0 || a.t_next == nullptr) {
+      // slices share the geometry: grouped items, one item per block; a
+      // single slice takes S = 1 (no clamped loads of absent slices)
+      constexpr int S = ORDER == 0 ? kDirectSlices0 : kDirectSlices1;
+      const int s = a.nt >= S ? S : 1;
+      const int nb = grid_blocks(ntx * bands * ((a.nt + s - 1) / s), 1, 1 << 24);
+      if (s == S)
+        hipLaunchKernelGGL((affine_direct_group_kernel<T, I, ORDER, RECOVER, S>), dim3(nb),
+                           dim3(kThreads), 0, st, args, ay, ax);
+      else
+        hipLaunchKernelGGL((affine_direct_group_kernel<T, I, ORDER, RECOVER, 1>), dim3(nb),
+                           dim3(kThreads), 0, st, args, ay, ax);
+    } else {   // order 1 with the zero-weight time neighbour: per slice
+      const int nb = grid_blocks(ntx * bands * a.nt, 1, 256 * 64);
+      hipLaunchKernelGGL((affine_direct_kernel<T, I, ORDER, RECOVER>), dim3(nb), dim3(kThreads),
+                         0, st, args, ay, ax);
+    }
     XRS_HIP_CHECK(hipGetLastError());
     return XRS_OK;
   }

@@ -67,10 +67,10 @@ struct BBoxArgs {
 // The claim-key scratch filled by K4's own grid: K4 reads the coordinates at
 // well under the HBM rate, so the writes ride along instead of taking a
 // memset pass of their own between K4 and the claim.  Non-temporal 16-byte
-// stores; kFillAt: 0 = all of a thread's share first, 1 = after its
-// blocks, 2 = a block's share of the scratch with each source block (the
-// block kernel; the per-pixel kernel fills first).
-constexpr int kFillAt = 2;
+// stores; the block kernel stores a block's share of the scratch with each
+// source block, the per-pixel kernel fills first.  (A fill on a side stream,
+// or of a thread's whole share before / after its blocks, measured slower:
+// DESIGN.md §3, round 4 (5).)
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ inline void fill_scratch(const BBoxArgs& a) {
@@ -382,7 +382,6 @@ template <bool SHARED>
 __global__ void __launch_bounds__(kThreads)
 ij_bboxes_block_kernel(BBoxArgs a) {
   extern __shared__ __align__(16) unsigned char smem[];
-  if (kFillAt == 0) fill_scratch(a);
   const int64_t nbx = 2 * a.ntx, nby = 2 * a.nty;
   double* sbx = reinterpret_cast<double*>(smem);
   double* sby = sbx + nbx;
@@ -425,7 +424,7 @@ ij_bboxes_block_kernel(BBoxArgs a) {
         y[r] = a.y[o];
       }
     }
-    if (kFillAt == 2 && a.fill) fill_scratch_block(a, blk, fill_per, lane);
+    if (a.fill) fill_scratch_block(a, blk, fill_per, lane);
     double xmn = x[0], xmx = x[0], ymn = y[0], ymx = y[0];
     bool nan = col_ok && (x[0] != x[0] || y[0] != y[0]);
 #pragma unroll
@@ -480,7 +479,6 @@ ij_bboxes_block_kernel(BBoxArgs a) {
       }
     }
   }
-  if (kFillAt == 1) fill_scratch(a);
   if (SHARED) {
     __syncthreads();
     for (int64_t k = threadIdx.x; k < a.nboxes; k += kThreads) {
@@ -851,13 +849,26 @@ __device__ inline double dpp_next_f64(double v) {   // lane i <- lane i + 1 (lan
   return __longlong_as_double((int64_t)(((uint64_t)hi << 32) | lo));
 }
 
-struct StripPoint {    // one source point of the strip
-  double x, y;
+__device__ inline float dpp_next_f32(float v) {      // lane i <- lane i + 1 (lane 63: 0)
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x130, 0xF, 0xF, true));
+}
+
+// trim_pad in float32 for the float32 window, widened by kPadEps32 (1 + sq):
+// the conversion of each q to float32 (<= 2^-24 |q|), the two subtractions
+// that place the window (<= 2^-24 (|q| + 1) each) and this expression's own
+// roundings (<= 6 ulps of a value below 1) together stay below it
+constexpr float kPadEps32 = 0x1p-20f;
+__device__ inline float trim_pad32(float qx0, float qx1, float qy0, float qy1, float sq, float d) {
+  return 8.0f * d * ((qx1 - qx0) + (qy1 - qy0)) + (1e-6f + kPadEps32) * (1.0f + sq);
+}
+
+struct PairQ {         // a point pair's extreme pixel units (float32); both finite
+  float xmn, xmx, ymn, ymx;
+  bool fin;
 };
 
-struct PairExt {       // a point pair's coordinate extremes; both points finite
-  double xmn, xmx, ymn, ymx;
-  bool fin;
+struct StripPoint {    // one source point of the strip
+  double x, y;
 };
 
 __device__ inline StripPoint strip_next(const StripPoint& p) {
@@ -998,14 +1009,17 @@ rectify_claim_kernel(RectArgs a) {
     auto qx = [&](double x) { return (x - ti.x_off) * a.inv_x; };
     auto qy = [&](double y) { return (y - ti.y_off) * a.inv_y; };
     StripPoint t0 = load_pt(ti.sj0 + r0);
-    // a row's point pairs (l, l + 1): their extremes and finiteness sum, for
-    // the quads above and below the row (computed once, not per quad)
-    auto pair_ext = [](const StripPoint& p, const StripPoint& q) {
-      const double sum = (p.x + q.x) + (p.y + q.y);   // NaN / inf if any is
-      return PairExt{fmin(p.x, q.x), fmax(p.x, q.x), fmin(p.y, q.y), fmax(p.y, q.y),
-                     sum - sum == 0.0};
+    // a row's point pairs (l, l + 1): the extremes of their tile-local pixel
+    // units in float32 (each point converted once, its right-hand neighbour's
+    // by DPP) and their finiteness, for the quads above and below the row
+    auto pair_q = [&](const StripPoint& p) {
+      const float ux = (float)qx(p.x), uy = (float)qy(p.y);
+      const float vx = dpp_next_f32(ux), vy = dpp_next_f32(uy);
+      const float sum = (ux + vx) + (uy + vy);   // NaN / inf if any is (or overflowed)
+      return PairQ{fminf(ux, vx), fmaxf(ux, vx), fminf(uy, vy), fmaxf(uy, vy),
+                   sum - sum == 0.0f};
     };
-    PairExt et = pair_ext(t0, strip_next(t0));
+    PairQ et = pair_q(t0);
     StripPoint nxt = load_pt(ti.sj0 + r0 + 1);
     for (int32_t r = r0; r < r_end; ++r) {
       const int32_t qj = ti.sj0 + r;                    // global quad row (corner p0)
@@ -1015,7 +1029,7 @@ rectify_claim_kernel(RectArgs a) {
       // the next row's bottom points are requested before this row's tests
       if (r + 1 < r_end) nxt = load_pt(qj + 2);
       const StripPoint b1 = strip_next(b0);
-      const PairExt eb = pair_ext(b0, b1);
+      const PairQ eb = pair_q(b0);
       // corners p0 = t0, p1 = t1, p2 = b0, p3 = b1
       int32_t imin = 0, jmin = 0, nw = 0;
       int64_t big_cnt = 0;   // > 0: window above kLaneWindow, walked by the wave below
@@ -1023,19 +1037,14 @@ rectify_claim_kernel(RectArgs a) {
       uint32_t hit = 0, hit_b = 0, unsure = 0;   // bit 2k: window pixel k (row-major) hit
                                                   // (hit_b: by triangle B) / undecided
       if (has_q) {
-        // floor is monotone and the reciprocal's error tiny: the extremes of the
-        // coordinates give the extreme pixel units
-        const double qx0 = qx(fmin(et.xmn, eb.xmn));
-        const double qx1 = qx(fmax(et.xmx, eb.xmx));
-        const double ylo = fmin(et.ymn, eb.ymn);
-        const double yhi = fmax(et.ymx, eb.ymx);
-        const double qy0 = qy(YPOS ? ylo : yhi);
-        const double qy1 = qy(YPOS ? yhi : ylo);
-
+        // the corners' extreme pixel units (float32, tile-local: |q| is at most
+        // a few tile widths for every quad the fast path takes)
+        const float qx0 = fminf(et.xmn, eb.xmn), qx1 = fmaxf(et.xmx, eb.xmx);
+        const float qy0 = fminf(et.ymn, eb.ymn), qy1 = fmaxf(et.ymx, eb.ymx);
         // sq >= every |q| (a sum, not a max: no NaN-quieting of the operands);
         // conditions combined with & (one branch, not one per term)
-        const double sq = (fabs(qx0) + fabs(qx1)) + (fabs(qy0) + fabs(qy1));
-        if (et.fin & eb.fin & (sq < 0x1p40)) {
+        const float sq = (fabsf(qx0) + fabsf(qx1)) + (fabsf(qy0) + fabsf(qy1));
+        if (et.fin & eb.fin & (sq < 0x1p20f)) {
           // T: the pixel centres (i + 0.5) within `pad` of the corners'
           // extremes, clipped to the tile — every other pixel is a miss of
           // both triangles (trim_pad).  With pad + the reciprocal's error
@@ -1044,29 +1053,40 @@ rectify_claim_kernel(RectArgs a) {
           // floor(q) and floor(q - 0.5 + pad) <= floor(q)), so R — its exact
           // floors — is needed only for the wave-wide walk of a large window
           // (R untrimmed) or a quad so large that pad >= 0.25.
-          const double d = fabs(a.uv_delta) + kMaxFormMargin * a.margin_scale;
-          const double pad = trim_pad(qx0, qx1, qy0, qy1, sq, d);
-          const double lo = 0.5 + pad, hi = 0.5 - pad;
-          const double ci = ceil(qx0 - lo), fi = floor(qx1 - hi);
-          const double cj = ceil(qy0 - lo), fj = floor(qy1 - hi);
-          const double twm1 = (double)(ti.tw - 1), thm1 = (double)(ti.th - 1);
-          const bool empty = !((ci <= fi) & (cj <= fj) & (fi >= 0.0) & (fj >= 0.0) &
+          // In float32: every q carries the rounding of its conversion
+          // (<= 2^-24 |q|) and the subtractions below round by <= 2^-24 (|q|
+          // + 1); the pad is widened by kPadEps32 (1 + sq) >= all of them
+          // together, so the float32 T holds every pixel of the float64 one.
+          const float d = (float)(fabs(a.uv_delta) + kMaxFormMargin * a.margin_scale);
+          const float pad = trim_pad32(qx0, qx1, qy0, qy1, sq, d);
+          const float lo = 0.5f + pad, hi = 0.5f - pad;
+          const float ci = ceilf(qx0 - lo), fi = floorf(qx1 - hi);
+          const float cj = ceilf(qy0 - lo), fj = floorf(qy1 - hi);
+          const float twm1 = (float)(ti.tw - 1), thm1 = (float)(ti.th - 1);
+          const bool empty = !((ci <= fi) & (cj <= fj) & (fi >= 0.0f) & (fj >= 0.0f) &
                                (ci <= twm1) & (cj <= thm1));
           int32_t ti0 = 0, ti1 = -1, tj0 = 0, tj1 = -1;
           if (!empty) {   // clipped to the tile by selects (values in range here)
-            ti0 = ci > 0.0 ? (int32_t)ci : 0;
-            tj0 = cj > 0.0 ? (int32_t)cj : 0;
+            ti0 = ci > 0.0f ? (int32_t)ci : 0;
+            tj0 = cj > 0.0f ? (int32_t)cj : 0;
             ti1 = fi < twm1 ? (int32_t)fi : ti.tw - 1;
             tj1 = fj < thm1 ? (int32_t)fj : ti.th - 1;
           }
           int64_t cnt = (int64_t)(ti1 - ti0 + 1) * (tj1 - tj0 + 1);
           bool walk = !empty;
           // (the exact-decision test knob sets an infinite margin: R always)
-          if (pad >= 0.25 || !(a.margin < 0.25) || (!empty && cnt > kLaneWindow)) {
+          if (pad >= 0.25f || !(a.margin < 0.25) || (!empty && cnt > kLaneWindow)) {
             walk = false;
+            // R from the float64 pixel units (rare: large windows / quads)
+            const double dqx0 = qx(fmin(fmin(t0.x, t1.x), fmin(b0.x, b1.x)));
+            const double dqx1 = qx(fmax(fmax(t0.x, t1.x), fmax(b0.x, b1.x)));
+            const double ylo = fmin(fmin(t0.y, t1.y), fmin(b0.y, b1.y));
+            const double yhi = fmax(fmax(t0.y, t1.y), fmax(b0.y, b1.y));
+            const double dqy0 = qy(YPOS ? ylo : yhi);
+            const double dqy1 = qy(YPOS ? yhi : ylo);
             double fx0, fx1, fy0, fy1;
-            if (floor_clear(qx0, a.margin, fx0) && floor_clear(qx1, a.margin, fx1) &&
-                floor_clear(qy0, a.margin, fy0) && floor_clear(qy1, a.margin, fy1)) {
+            if (floor_clear(dqx0, a.margin, fx0) && floor_clear(dqx1, a.margin, fx1) &&
+                floor_clear(dqy0, a.margin, fy0) && floor_clear(dqy1, a.margin, fy1)) {
               int32_t i0 = (int32_t)fx0, i1 = (int32_t)fx1, j0 = (int32_t)fy0, j1 = (int32_t)fy1;
               if (!empty && !(i1 < 0 || j1 < 0 || i0 >= ti.tw || j0 >= ti.th)) {
                 i0 = max(i0, 0); j0 = max(j0, 0);
