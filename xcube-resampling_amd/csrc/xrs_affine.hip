@@ -316,6 +316,28 @@ __device__ inline void store_value(const AffineArgs& a, int64_t didx, I v) {
   else store_any(a.dst, didx, a.dst_dtype, 0.0, (int64_t)v, true);
 }
 
+// The output dtype code of an intermediate type (K2's output dtype is its
+// intermediate dtype for every plan the host makes: plain affine and the
+// first / last / center picks keep it; anything else takes store_any).
+template <typename I> constexpr int dtype_code() {
+  return std::is_same<I, float>::value ? XRS_DTYPE_F32 : std::is_same<I, double>::value ? XRS_DTYPE_F64
+       : std::is_same<I, uint8_t>::value ? XRS_DTYPE_U8 : std::is_same<I, int8_t>::value ? XRS_DTYPE_I8
+       : std::is_same<I, uint16_t>::value ? XRS_DTYPE_U16 : std::is_same<I, int16_t>::value ? XRS_DTYPE_I16
+       : std::is_same<I, uint32_t>::value ? XRS_DTYPE_U32 : std::is_same<I, int32_t>::value ? XRS_DTYPE_I32
+       : std::is_same<I, int64_t>::value ? XRS_DTYPE_I64 : 0;
+}
+
+template <typename I>
+__device__ inline void store_typed(const AffineArgs& a, int64_t didx, I v) {
+  if (a.dst_dtype == dtype_code<I>()) {   // wave-uniform
+    I* d = static_cast<I*>(a.dst) + didx;
+    if (std::is_floating_point<I>::value) __builtin_nontemporal_store(v, d);
+    else *d = v;
+  } else {
+    store_value<I>(a, didx, v);
+  }
+}
+
 __device__ inline int32_t wave_uniform(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
 // K2 (no reduction: plain affine, or coarsen first/last/center which pick ONE
@@ -345,29 +367,7 @@ __device__ inline void direct_rows(const AffineArgs& a, const AxisChunks& ay, co
   for (int q = 0; q < kDirectRows; ++q) {
     if (oj0 + q >= a.out_h) break;
     const I v = tp[q].template eval<I, ORDER, RECOVER, HAS_T1>(ey[q], ex, a.cval);
-    store_value<I>(a, t * a.dst_st + (oj0 + q) * a.dst_sy + oi, v);
-  }
-}
-
-// The output dtype code of an intermediate type (K2's output dtype is its
-// intermediate dtype for every plan the host makes: plain affine and the
-// first / last / center picks keep it; anything else takes store_any).
-template <typename I> constexpr int dtype_code() {
-  return std::is_same<I, float>::value ? XRS_DTYPE_F32 : std::is_same<I, double>::value ? XRS_DTYPE_F64
-       : std::is_same<I, uint8_t>::value ? XRS_DTYPE_U8 : std::is_same<I, int8_t>::value ? XRS_DTYPE_I8
-       : std::is_same<I, uint16_t>::value ? XRS_DTYPE_U16 : std::is_same<I, int16_t>::value ? XRS_DTYPE_I16
-       : std::is_same<I, uint32_t>::value ? XRS_DTYPE_U32 : std::is_same<I, int32_t>::value ? XRS_DTYPE_I32
-       : std::is_same<I, int64_t>::value ? XRS_DTYPE_I64 : 0;
-}
-
-template <typename I>
-__device__ inline void store_typed(const AffineArgs& a, int64_t didx, I v) {
-  if (a.dst_dtype == dtype_code<I>()) {   // wave-uniform
-    I* d = static_cast<I*>(a.dst) + didx;
-    if (std::is_floating_point<I>::value) __builtin_nontemporal_store(v, d);
-    else *d = v;
-  } else {
-    store_value<I>(a, didx, v);
+    store_typed<I>(a, t * a.dst_st + (oj0 + q) * a.dst_sy + oi, v);
   }
 }
 
@@ -986,19 +986,15 @@ int launch(const AffineArgs& a, const AxisChunks& ay, const AxisChunks& ax, Axis
   if (direct) {   // one launch: the kernel evaluates its two table entries inline
     const int64_t bands = (a.out_h + kTileH * kDirectRows - 1) / (kTileH * kDirectRows);
     const int64_t ntx = (a.out_w + kTileW - 1) / kTileW;
-    if (ORDER == 0 || a.t_next == nullptr) {
-      // slices share the geometry: grouped items, one item per block; a
-      // single slice takes S = 1 (no clamped loads of absent slices)
-      constexpr int S = ORDER == 0 ? kDirectSlices0 : kDirectSlices1;
-      const int s = a.nt >= S ? S : 1;
-      const int nb = grid_blocks(ntx * bands * ((a.nt + s - 1) / s), 1, 1 << 24);
-      if (s == S)
-        hipLaunchKernelGGL((affine_direct_group_kernel<T, I, ORDER, RECOVER, S>), dim3(nb),
-                           dim3(kThreads), 0, st, args, ay, ax);
-      else
-        hipLaunchKernelGGL((affine_direct_group_kernel<T, I, ORDER, RECOVER, 1>), dim3(nb),
-                           dim3(kThreads), 0, st, args, ay, ax);
-    } else {   // order 1 with the zero-weight time neighbour: per slice
+    constexpr int S = ORDER == 0 ? kDirectSlices0 : kDirectSlices1;
+    if ((ORDER == 0 || a.t_next == nullptr) && a.nt >= S) {
+      // slices share the geometry: grouped items, one item per block
+      const int nb = grid_blocks(ntx * bands * ((a.nt + S - 1) / S), 1, 1 << 24);
+      hipLaunchKernelGGL((affine_direct_group_kernel<T, I, ORDER, RECOVER, S>), dim3(nb),
+                         dim3(kThreads), 0, st, args, ay, ax);
+    } else {   // fewer slices than a group (config 1: one chunk, 7.2 us against
+               // 7.7 us grouped with S = 1), or order 1 with the zero-weight
+               // time neighbour: per slice
       const int nb = grid_blocks(ntx * bands * a.nt, 1, 256 * 64);
       hipLaunchKernelGGL((affine_direct_kernel<T, I, ORDER, RECOVER>), dim3(nb), dim3(kThreads),
                          0, st, args, ay, ax);
