@@ -117,7 +117,8 @@ N_SIMD = 1024   # 256 CUs x 4 SIMDs
 N_XCD = 8
 
 
-def issue_pmc(kernels=("claim", "resolve", "ij_bboxes"), timeout=150):
+def issue_pmc(kernels=("claim", "resolve", "ij_bboxes"), timeout=150,
+              script=("time_rectify.py", "--fused", "--reps", "3")):
     """Per kernel: VALU-issue fraction = 4 x SQ_ACTIVE_INST_VALU (quad-cycles
     of VALU issue, summed over the SIMDs) / (N_SIMD x GRBM_GUI_ACTIVE / N_XCD
     (the dispatch's shader cycles; the GRBM counter sums the 8 XCDs)): the
@@ -139,8 +140,7 @@ def issue_pmc(kernels=("claim", "resolve", "ij_bboxes"), timeout=150):
     try:
         cmd = ["timeout", "-s", "KILL", str(timeout), prof, "--pmc", *ISSUE_COUNTERS,
                "--kernel-trace", "--output-format", "csv", "-d", d, "-o", "p", "--",
-               sys.executable, os.path.join(ROOT, "scripts", "time_rectify.py"), "--fused",
-               "--reps", "3"]
+               sys.executable, os.path.join(ROOT, "scripts", script[0]), *script[1:]]
         r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
         if r.returncode != 0:
             print(f"issue_pmc: rocprofv3 failed (rc {r.returncode}):\n{r.stdout[-1500:]}",
@@ -169,8 +169,8 @@ def issue_pmc(kernels=("claim", "resolve", "ij_bboxes"), timeout=150):
                       "wait_frac": round(c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"], 4)
                       if c["SQ_WAVE_CYCLES"] else None,
                       "shader_cycles": int(cyc), "dispatches": n}
-        out["method"] = ("rocprofv3 --pmc " + " ".join(ISSUE_COUNTERS) + " on scripts/"
-                         "time_rectify.py --fused (the config-4 pass): valu_issue_frac = 4 x "
+        out["method"] = ("rocprofv3 --pmc " + " ".join(ISSUE_COUNTERS) + " on scripts/" +
+                         " ".join(script) + ": valu_issue_frac = 4 x "
                          "SQ_ACTIVE_INST_VALU / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs); "
                          "wait_frac = SQ_WAIT_ANY / SQ_WAVE_CYCLES")
         return out
@@ -339,13 +339,17 @@ def config2u(args):
     flags.raise_if_set("config 2u fused")
     assert torch.equal(torch.nan_to_num(fout, nan=-7.0), torch.nan_to_num(out, nan=-7.0)), \
         "config 2u: fused gather differs from the tables path"
+    torch.cuda.synchronize()
+    # the transformation is f64-VALU bound: its issue fractions (2u-fused's roof)
+    issue = issue_pmc(kernels=("gather_proj_kernel", "transform_kernel", "gather_2d_kernel"),
+                      script=("time_2u.py", "--reps", "3"))
     _line("2u-fused", "reproject bilinear 8192x8192 f32 UTM 32N (EPSG:32632) -> LAEA Europe "
                       "(EPSG:3035) 30 m, 2048^2 tiles, f64 out; transformation fused into the "
                       "gather (xrs_reproject_proj), bit-identical to the tables path",
           size * size, f_ms, f_wall, 8 * size * size + 4 * size * size,
           "gather_proj_kernel<LAEA_INV, TMERC_FWD>",
           dict(value=round(cpu_v, 2), unit="Mpixels/s", cores=cores, kind="port",
-               sample="as the 2u line"), {"covered_px": covered})
+               sample="as the 2u line"), {"covered_px": covered, "issue": issue})
 
 
 # ------------------------------------------------------------------ config 3

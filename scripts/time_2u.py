@@ -1,0 +1,47 @@
+"""Config-2u kernels run a few times each (xrs_transform + K1c on the 2-D
+tables, and the fused gather xrs_reproject_proj): the workload of
+scripts/bench_configs.py config2u, for rocprofv3 counter passes.
+    python scripts/time_2u.py [--reps N]"""
+from __future__ import annotations
+
+import argparse
+import dataclasses
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=3)
+    args = ap.parse_args()
+    import torch
+
+    import xcube_resampling_amd as xrs
+    from xcube_resampling_amd import kernels
+
+    size, res = 8192, 30.0
+    sgm = xrs.GridMapping.regular((size, size), (400000.0, 5400000.0), res, "EPSG:32632",
+                                  tile_size=2048)
+    tgm = xrs.GridMapping.regular((size, size), (4180000.0, 2870000.0), res, "EPSG:3035",
+                                  tile_size=2048)
+    tr = xrs.Transformer.from_crs(tgm.crs, sgm.crs, always_xy=True)
+    plan = xrs.plan_reproject(sgm, tgm, tr)
+    src = torch.rand((1, size, size), device="cuda", dtype=torch.float32)
+    out = torch.empty((1, size, size), device="cuda", dtype=torch.float64)
+    flags = kernels.ErrorFlags(src.device)
+    fplan = dataclasses.replace(plan, fuse_transform=True, _device_cache={})
+    for _ in range(args.reps):
+        plan._device_cache.clear()
+        kernels.reproject(src, plan, "bilinear", float("nan"), out=out, flags=flags, check=False)
+        kernels.reproject(src, fplan, "bilinear", float("nan"), out=out, flags=flags,
+                          check=False)
+    torch.cuda.synchronize()
+    flags.raise_if_set("time_2u")
+    print("time_2u done", flush=True)
+
+
+if __name__ == "__main__":
+    main()
