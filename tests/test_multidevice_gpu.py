@@ -209,3 +209,66 @@ def test_rectify_devices_reference_goldens_and_device_data():
     out = xrs.resample_in_space(ds, target_gm=tgm, interp_methods=0, devices=[0, 0])
     assert out["rad"].data.is_cuda
     np.testing.assert_almost_equal(out["rad"].data.cpu().numpy(), gold)
+
+
+def test_devices_non_separable_reprojection():
+    """A non-separable pair (LAEA source -> geographic, the reference's
+    test_reproject_complex_dask_array case: 2-D coordinate tables made on
+    each device, row bands balanced by rows) over two and three parts ==
+    the single-device call; and one variable, whose plan fuses the
+    transformation into the gather."""
+    import xcube_resampling_amd as xrs
+    from fixtures import dataset_large_for_reproject
+
+    tgm = xrs.GridMapping.regular((10, 10), (6.0, 48.0), 0.2, "EPSG:4326", tile_size=(5, 5))
+    src = dataset_large_for_reproject()
+    # two yx variables: the plan keeps 2-D coordinate tables (one per device)
+    src["t2"] = xrs.DataArray(src["temperature"].values[:3] * 2.0, ("time2", "y", "x"))
+    for interp in ("nearest", "triangular", "bilinear"):
+        one = xrs.reproject_dataset(src, tgm, interp_methods=interp)
+        for devices in ([0, 0], [0, 0, 0]):
+            many = xrs.reproject_dataset(src, tgm, interp_methods=interp, devices=devices)
+            for k in ("temperature", "t2"):
+                assert_bitwise_equal(many[k].values, one[k].values,
+                                     f"{interp}/{k}/{len(devices)}")
+    # one yx variable: the transformation fused into the gather
+    one = xrs.reproject_dataset(dataset_large_for_reproject(), tgm, interp_methods=1)
+    two = xrs.reproject_dataset(dataset_large_for_reproject(), tgm, interp_methods=1,
+                                devices=[0, 0])
+    assert_bitwise_equal(two["temperature"].values, one["temperature"].values, "fused")
+
+
+def test_devices_affine_order1_time_neighbours():
+    """Order-1 3-D affine with dask-image's zero-weight time neighbour (the
+    per-slice kernel path) split into output row bands over two parts, NaN
+    in the data == the oracle."""
+    import xcube_resampling_amd.affine as A
+    from oracle import affine_ref
+    from xcube_resampling_amd import multidevice
+
+    rng = np.random.default_rng(12)
+    a = rng.random((3, 300, 260)).astype(np.float32)
+    a.ravel()[rng.random(a.size) < 0.002] = np.nan
+    m = ((0.7, 0.0, 3.3), (0.0, 0.8, 1.5))
+    oshape, ochunks = (3, 240, 200), (2, 64, 64)
+    ref = affine_ref.resample_array(a, m, oshape, ochunks, 1, "first", False, np.nan)
+    with multidevice.use_devices([0, 0]):
+        got = A._resample_array(a, None, None, m, oshape, ochunks, 1, "first", False, np.nan)
+    assert_bitwise_equal(got, np.asarray(ref), "order 1, time neighbours")
+
+
+def test_devices_more_parts_than_rows():
+    """More devices than target rows / tiles: the extra parts get empty
+    shards and the result is unchanged (reproject, rectify)."""
+    import xcube_resampling_amd as xrs
+
+    g = load_golden("reproject_f32.npz")
+    ds, tgm = reproject_golden_inputs(g)
+    many = xrs.reproject_dataset(ds, tgm, interp_methods="nearest",
+                                 devices=[0] * (tgm.height + 3))
+    assert_bitwise_equal(many["v"].values, g["out_nearest"], "reproject")
+    gold = reference_goldens("tests/test_rectify.py")["__helpers__"]["expected_rad_13x13"]
+    rtgm = xrs.GridMapping.regular((13, 13), (-0.25, 49.75), 0.5, "EPSG:4326", tile_size=5)
+    out = xrs.rectify_dataset(dataset_2x2_irregular(), target_gm=rtgm, interp_methods=0,
+                              devices=[0] * 12)
+    np.testing.assert_almost_equal(out["rad"].values, gold)

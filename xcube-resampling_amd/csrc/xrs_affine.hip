@@ -109,29 +109,33 @@ __device__ inline bool integral_entry(const AxisTab& e, int32_t g_first, int k) 
          (ORDER == 0 || (e.w1 == 0.0 && e.g1 == e.g0 + 1));
 }
 
-// With `nonint` (K3i candidates, div dy x dx): also count the in-bounds entries
-// that break the integral-contiguous layout K3i's fast path needs (entry k of
-// a pixel's run = first entry + k, order 1: weight 0 and the next tap at +1).
-// The image's last row / column (scipy mirrors the tap past it) always breaks
-// it; K3i serves such pixels through its exact path, so a few broken entries
-// still select K3i (`integral_limit`).
+// With `runs` (K3i candidates, div dy x dx): also K3i's run records — per
+// output row / column the first source index of its integral-contiguous run
+// of entries (entry k of a pixel's run = first entry + k, order 1: weight 0
+// and the next tap at +1), -1 where the layout breaks (the image's last row /
+// column, where scipy mirrors the tap, always breaks it: K3i serves such
+// pixels through its exact path).  Block 0 also sets K3i's counters: the
+// slow-pixel count to 0 and — with time neighbours — whether any slice's
+// zero-weight neighbour is another slice (plain stores: no memset before
+// this launch; K3i and its finish run after it on the same stream).
 template <int ORDER>
 __global__ void __launch_bounds__(kThreads)
 affine_tables_kernel(AxisChunks ay, AxisChunks ax, AxisTab* __restrict__ ytab,
                      AxisTab* __restrict__ xtab, int64_t dy, int64_t dx,
-                     int32_t* __restrict__ nonint, const int64_t* __restrict__ t_next,
-                     int64_t nt, int32_t* __restrict__ nonself, int32_t* __restrict__ yrun,
+                     int32_t* __restrict__ counters, const int64_t* __restrict__ t_next,
+                     int64_t nt, bool check_self, int32_t* __restrict__ yrun,
                      int32_t* __restrict__ xrun) {
-  // K3i: does any slice have a zero-weight time neighbour other than itself?
-  if (nonself) {
-    bool other = false;
-    for (int64_t t = (int64_t)blockIdx.x * kThreads + threadIdx.x; t < nt;
-         t += (int64_t)gridDim.x * kThreads)
-      other = other || t_next[t] != t;
-    if (__any(other) && (threadIdx.x & 63) == 0) atomicOr(nonself, 1);
+  if (counters && blockIdx.x == 0) {
+    bool other = false;   // K3i: a zero-weight time neighbour other than the slice?
+    if (check_self)
+      for (int64_t t = threadIdx.x; t < nt; t += kThreads) other = other || t_next[t] != t;
+    const int any = __syncthreads_or(other);
+    if (threadIdx.x == 0) {
+      counters[1] = any ? 1 : 0;
+      counters[2] = 0;   // K3i's slow-pixel count
+    }
   }
   const int64_t total = ay.n + ax.n;
-  bool broken = false;
   for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * kThreads) {
     const bool is_y = i < ay.n;
@@ -139,23 +143,13 @@ affine_tables_kernel(AxisChunks ay, AxisChunks ax, AxisTab* __restrict__ ytab,
     const AxisChunks& ac = is_y ? ay : ax;
     const AxisTab e = axis_entry<ORDER>(ac, o);
     (is_y ? ytab : xtab)[o] = e;
-    if (nonint && e.g0 >= 0) {
-      const int64_t d = is_y ? dy : dx, k = o % d;
-      const AxisTab f = k ? axis_entry<ORDER>(ac, o - k) : e;
-      broken = broken || f.g0 < 0 || !integral_entry<ORDER>(e, f.g0, (int)k);
-      if (k == 0) {   // K3i's run record of output row / column o / d
-        bool ok = integral_entry<ORDER>(e, e.g0, 0);
-        for (int64_t j = 1; j < d && ok; ++j)
-          ok = integral_entry<ORDER>(axis_entry<ORDER>(ac, o + j), e.g0, (int)j);
-        (is_y ? yrun : xrun)[o / d] = ok ? e.g0 : -1;
-      }
-    } else if (nonint && o % (is_y ? dy : dx) == 0) {
-      (is_y ? yrun : xrun)[o / (is_y ? dy : dx)] = -1;
+    const int64_t d = is_y ? dy : dx;
+    if (counters && o % d == 0) {   // K3i's run record of output row / column o / d
+      bool ok = e.g0 >= 0 && integral_entry<ORDER>(e, e.g0, 0);
+      for (int64_t j = 1; j < d && ok; ++j)
+        ok = integral_entry<ORDER>(axis_entry<ORDER>(ac, o + j), e.g0, (int)j);
+      (is_y ? yrun : xrun)[o / d] = ok ? e.g0 : -1;
     }
-  }
-  if (nonint) {   // count of broken entries (one atomic per wave)
-    const int nbroken = __popcll(__ballot(broken));
-    if (nbroken && (threadIdx.x & 63) == 0) atomicAdd(nonint, nbroken);
   }
 }
 
@@ -693,10 +687,8 @@ template <typename T, int ORDER, int D, bool TWO>
 __global__ void __launch_bounds__(kThreads)
 affine_reduce_integral_kernel(AffineArgs a, const int32_t* __restrict__ yrun,
                               const int32_t* __restrict__ xrun,
-                              const int32_t* __restrict__ nonint, int32_t nonint_limit,
                               const int32_t* __restrict__ nonself, int32_t* __restrict__ nslow,
                               int64_t* __restrict__ slow_list, int64_t slow_cap) {
-  if (*nonint > nonint_limit) return;   // the generic K3 launched beside this one works
   // with time neighbours: the TWO=false instance serves launches where every
   // neighbour is the slice itself (its taps are the ones already checked)
   if (nonself && TWO != (*nonself != 0)) return;
@@ -714,6 +706,9 @@ affine_reduce_integral_kernel(AffineArgs a, const int32_t* __restrict__ yrun,
   // time.  Dealing each XCD one contiguous eighth of the image instead (eight
   // separate runs in flight) took 0.231 vs 0.222 ms at config 3, items dealt
   // one by one 0.261 ms (profiles/r04_k3_ab.log).
+  // the slow list overflowed (seen by this wave): a grid off the integral
+  // layout, which the finish hands to the generic K3 — stop appending
+  bool full = false;
   for (XcdGroups sg = xcd_groups(nwork, ntx);; sg.i += sg.step) {
     const int64_t w = sg.item();
     if (w >= nwork) break;
@@ -741,6 +736,7 @@ affine_reduce_integral_kernel(AffineArgs a, const int32_t* __restrict__ yrun,
     const int32_t gf = __builtin_amdgcn_readfirstlane(el);   // lane 0's: scalar row math
     const uint64_t okm = __ballot(lane < nrows && el >= 0 && el == gf + lane * D);
     const int nfast = __builtin_ctzll(~okm);   // leading rows (R < 64)
+    // (rows off the integral layout load nothing: nfast = 0)
     const bool rows_fast = nfast > 0;
     const bool fast = rows_fast && col_fast;
     // loads are unconditional (a branch per row would serialise them): lanes
@@ -787,6 +783,7 @@ affine_reduce_integral_kernel(AffineArgs a, const int32_t* __restrict__ yrun,
         }
       }
     }
+    bool overflow = false;
 #pragma unroll
     for (int q = 0; q < R; ++q) {
       if (q >= nrows) break;
@@ -854,8 +851,11 @@ affine_reduce_integral_kernel(AffineArgs a, const int32_t* __restrict__ yrun,
       }
       if (slow) {   // the exact path runs in integral_slow_kernel (keeps its
                     // registers out of this streaming kernel)
-        const int32_t k = atomicAdd(nslow, 1);
-        if (k < slow_cap) slow_list[k] = (t * a.out_h + oj) * a.out_w + oi;
+        if (!full) {
+          const int32_t k = atomicAdd(nslow, 1);
+          if (k < slow_cap) slow_list[k] = (t * a.out_h + oj) * a.out_w + oi;
+          else overflow = true;
+        }
         continue;
       }
       Fold<T> fold;
@@ -867,6 +867,7 @@ affine_reduce_integral_kernel(AffineArgs a, const int32_t* __restrict__ yrun,
         });
       fold.store(a, didx);
     }
+    full = full || __any(overflow);
   }
 }
 
@@ -929,10 +930,10 @@ template <typename T, int ORDER, int D>
 __global__ void __launch_bounds__(kThreads)
 integral_finish_kernel(AffineArgs a, const AxisTab* __restrict__ ytab,
                        const AxisTab* __restrict__ xtab, int group,
-                       const int32_t* __restrict__ nonint, int32_t nonint_limit,
+                       const int32_t* __restrict__ counters,
                        const int64_t* __restrict__ slow_list, int64_t slow_cap) {
-  const int64_t n = nonint[2];
-  if (nonint[0] <= nonint_limit && n <= slow_cap) slow_body<T, ORDER, D>(a, ytab, xtab, slow_list, n);
+  const int64_t n = counters[2];
+  if (n < slow_cap) slow_body<T, ORDER, D>(a, ytab, xtab, slow_list, n);
   else reduce_body<T, T, ORDER, false>(a, ytab, xtab, group);
 }
 
@@ -946,8 +947,10 @@ inline int64_t reduce_row_bytes(int64_t dx, int64_t isize) {
 
 // K3i candidates: square 2/4/8 coarsen factors of float rasters.  Whether the
 // tables really are integral is known on the device only (affine_tables_kernel
-// sets `nonint`), so K3i and the generic K3 are both launched and exactly one
-// of them works (the other returns at its first instruction).
+// writes the run records), so K3i and its finish are launched; the finish runs
+// the slow pixels K3i listed, or the generic K3 over the whole launch when the
+// list overflowed (a grid off the integral layout: K3i then stops loading as
+// soon as the list is full).
 // xrs_testing_set(XRS_TESTING_AFFINE_GENERIC, 1) forces the generic K3 (tests).
 template <typename T, typename I, bool RECOVER>
 inline bool integral_candidate(const AffineArgs& a) {
@@ -957,14 +960,10 @@ inline bool integral_candidate(const AffineArgs& a) {
   return xrs_testing_value(XRS_TESTING_AFFINE_GENERIC) == 0;
 }
 
-// Broken table entries K3i still takes (each costs its pixels the exact
-// path): the image edges plus a little; a grid off the integral layout (a
-// fractional offset) breaks nearly every entry and runs the generic K3.
+// Slow pixels K3i lists (each takes the exact path): the image edges plus a
+// little; a grid off the integral layout makes nearly every pixel slow and
+// overflows the list, which hands the launch to the generic K3.
 inline int64_t slow_capacity(int64_t ih, int64_t iw) { return 4 * (ih + iw) + 1024; }
-
-inline int32_t integral_limit(int64_t ih, int64_t iw) {
-  return (int32_t)std::min<int64_t>(INT32_MAX, 64 + (ih + iw) / 64);
-}
 
 template <typename T, typename I, int ORDER, bool RECOVER>
 int launch(const AffineArgs& a, const AxisChunks& ay, const AxisChunks& ax, AxisTab* ytab,
@@ -972,12 +971,11 @@ int launch(const AffineArgs& a, const AxisChunks& ay, const AxisChunks& ax, Axis
   const bool direct = a.agg == AGG_NONE || a.agg == AGG_FIRST || a.agg == AGG_LAST ||
                       a.agg == AGG_CENTER;
   const bool k3i = !direct && integral_candidate<T, I, RECOVER>(a);
-  const int32_t limit = integral_limit(ay.n, ax.n);
-  // nonint[0]: broken entry count, nonint[1]: a time neighbour other than the slice
-  // nonint[2]: K3i's slow-pixel count (list of slow_cap entries after the flags)
-  // (one slice: its only possible neighbour is itself -> the TWO=false instance)
+  // counters (set by the tables kernel, no memset): nonint[1] a time neighbour
+  // other than the slice, nonint[2] K3i's slow-pixel count (list of slow_cap
+  // entries after them); one slice: its only possible neighbour is itself ->
+  // the TWO=false instance
   const bool t1_flag = k3i && ORDER == 1 && a.t_next != nullptr && a.nt > 1;
-  if (k3i) XRS_HIP_CHECK(hipMemsetAsync(nonint, 0, 4 * sizeof(int32_t), st));
   int64_t* slow_list = reinterpret_cast<int64_t*>(nonint + 4);
   const int64_t slow_cap = slow_capacity(ay.n, ax.n);
   AffineArgs args = a;
@@ -1008,7 +1006,7 @@ int launch(const AffineArgs& a, const AxisChunks& ay, const AxisChunks& ax, Axis
   int32_t* xrun = yrun + a.out_h;
   hipLaunchKernelGGL((affine_tables_kernel<ORDER>), dim3(nbt), dim3(kThreads), 0, st, ay, ax,
                      ytab, xtab, a.dy, a.dx, k3i ? nonint : nullptr, a.t_next, a.nt,
-                     t1_flag ? nonint + 1 : nullptr, yrun, xrun);
+                     t1_flag, yrun, xrun);
   XRS_HIP_CHECK(hipGetLastError());
   if (k3i) {
     const int64_t ntiles = ((a.out_w + kThreads - 1) / kThreads) *
@@ -1020,8 +1018,8 @@ int launch(const AffineArgs& a, const AxisChunks& ay, const AxisChunks& ax, Axis
     if constexpr (std::is_floating_point<T>::value && std::is_same<T, I>::value && !RECOVER) {
 #define XRS_K3I(D, TWO, SELF)                                                             \
   hipLaunchKernelGGL((affine_reduce_integral_kernel<T, ORDER, D, TWO>), dim3(nb),         \
-                     dim3(kThreads), 0, st, args, yrun, xrun, nonint, limit, SELF,       \
-                     nonint + 2, slow_list, slow_cap)
+                     dim3(kThreads), 0, st, args, yrun, xrun, SELF, nonint + 2,          \
+                     slow_list, slow_cap)
       // with time neighbours both instances launch; nonint[1] picks one
       constexpr bool O1 = ORDER == 1;
       int32_t* self = t1_flag ? nonint + 1 : nullptr;
@@ -1054,8 +1052,8 @@ int launch(const AffineArgs& a, const AxisChunks& ay, const AxisChunks& ax, Axis
 #define XRS_K3F(D)                                                                           \
   do {                                                                                       \
     hipLaunchKernelGGL((integral_finish_kernel<T, ORDER, D>), dim3(nb), dim3(kThreads),      \
-                       (size_t)band, st, args, ytab, xtab, (int)group, nonint, limit,        \
-                       slow_list, slow_cap);                                                 \
+                       (size_t)band, st, args, ytab, xtab, (int)group, nonint, slow_list,    \
+                       slow_cap);                                                            \
     launched = true;                                                                         \
   } while (0)
       if (a.dx == 2) XRS_K3F(2);
