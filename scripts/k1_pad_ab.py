@@ -53,8 +53,15 @@ def main():
         step()
     e1.record(stream)
     torch.cuda.synchronize()
+    # a checksum of the raster's bit patterns (arms must agree bit for bit)
+    csum = 0
+    for r in range(0, 40960, 4096):
+        v = out[0, r:r + 4096].view(torch.int32)
+        csum = (csum + int(v.sum(dtype=torch.int64)) * (r // 4096 + 1)) % (1 << 61)
+    flags.raise_if_set("k1 arm")
     print(json.dumps({"tag": args.tag, "pad_mb": args.pad_mb, "src_ptr": hex(src.data_ptr()),
-                      "out_ptr": hex(out.data_ptr()), "ms_per_launch": round(e0.elapsed_time(e1) / args.steps, 4)}))
+                      "out_ptr": hex(out.data_ptr()), "ms_per_launch": round(e0.elapsed_time(e1) / args.steps, 4),
+                      "checksum": csum}))
     del pad
 
 
