@@ -196,3 +196,58 @@ def test_reproject_plans_use_column_generators():
     plan2 = xrs.plan_reproject(sgm, utm, xrs.Transformer.from_crs(utm.crs, sgm.crs,
                                                                    always_xy=True))
     assert plan2.coord_mode == 1 and plan2.x_gen is None
+
+
+@pytest.mark.parametrize("crs_pair", [("EPSG:3857", "EPSG:4326"), ("EPSG:4326", "EPSG:3857"),
+                                      ("EPSG:3035", "EPSG:32632"), ("EPSG:32632", "EPSG:3035"),
+                                      ("EPSG:4326", "EPSG:4326")])
+def test_transform_bounds_many_equals_tile_by_tile(crs_pair):
+    """plan_reproject's vectorised source bounds (one transform of every
+    tile's densified edges) equal transform_bounds tile by tile, bit for bit,
+    including tiles whose points are all outside the projection (inf)."""
+    import xcube_resampling_amd as xrs
+
+    tr = xrs.Transformer.from_crs(crs_pair[0], crs_pair[1], always_xy=True)
+    rng = np.random.default_rng(7)
+    if crs_pair[0] == "EPSG:3857":
+        lo, hi, span = -2.0e7, 2.0e7, 4.0e5
+    elif crs_pair[0] == "EPSG:4326":
+        lo, hi, span = -80.0, 80.0, 3.0
+    else:
+        lo, hi, span = 2.0e5, 6.0e6, 2.0e5
+    x0 = rng.uniform(lo, hi, 64)
+    y0 = rng.uniform(lo, hi, 64) if crs_pair[0] != "EPSG:4326" else rng.uniform(-80, 80, 64)
+    w = rng.uniform(0.1, 1.0, 64) * span
+    bb = np.stack([x0, y0, x0 + w, y0 + w], axis=1)
+    if crs_pair[0] == "EPSG:3857":
+        bb[0] = [1e30, 1e30, 2e30, 2e30]   # nothing finite
+    with np.errstate(over="ignore", invalid="ignore"):
+        many = tr.transform_bounds_many(bb)
+        one = np.array([tr.transform_bounds(*b) for b in bb])
+    assert many.shape == one.shape
+    np.testing.assert_array_equal(many.view(np.int64), one.view(np.int64))
+
+
+def test_plan_bboxes_vectorised_equal_per_tile_loop():
+    """The config-5 plan's tile windows through the vectorised bounds equal
+    the per-tile computation (reproject.py:385-403)."""
+    import bench
+
+    sgm, tgm, plan, _, _ = bench.workload(8192, 2048)
+    import xcube_resampling_amd as xrs
+
+    tr = xrs.Transformer.from_crs(tgm.crs, sgm.crs, always_xy=True)
+    origin = sgm.x_coords.values[0], sgm.y_coords.values[0]
+    exp = []
+    for xy_bbox in tgm.xy_bboxes:
+        sb = tr.transform_bounds(*xy_bbox)
+        exp.append([math.floor((sb[0] - origin[0]) / sgm.x_res),
+                    math.floor((origin[1] - sb[3]) / sgm.y_res),
+                    math.ceil((sb[2] - origin[0]) / sgm.x_res),
+                    math.ceil((origin[1] - sb[1]) / sgm.y_res)])
+    exp = np.array(exp)
+    i_diff, j_diff = exp[:, 2] - exp[:, 0], exp[:, 3] - exp[:, 1]
+    i_start = exp[:, 0] - (i_diff.max() + 1 - i_diff) // 2
+    j_start = exp[:, 1] - (j_diff.max() + 1 - j_diff) // 2
+    np.testing.assert_array_equal(plan.tile_win, np.stack([i_start, j_start], axis=1))
+    assert plan.win_width == i_diff.max() + 1 and plan.win_height == j_diff.max() + 1

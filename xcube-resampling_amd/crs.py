@@ -588,3 +588,30 @@ class Transformer:
             return (math.inf, math.inf, math.inf, math.inf)
         tx, ty = tx[ok], ty[ok]
         return (float(tx.min()), float(ty.min()), float(tx.max()), float(ty.max()))
+
+    def transform_bounds_many(self, bboxes, densify_pts: int = 21):
+        """transform_bounds for an (N, 4) array of (left, bottom, right, top),
+        in one vectorised pass: the same densified points (element for
+        element the same float64 operations) and the same min / max, as an
+        (N, 4) array; rows with no finite point are inf."""
+        b = np.asarray(bboxes, dtype=np.float64).reshape(-1, 4)
+        left, bottom, right, top = (b[:, i:i + 1] for i in range(4))
+        side = densify_pts + 1
+        dx = (right - left) / side
+        dy = (top - bottom) / side
+        k = np.arange(side, dtype=np.float64)[None, :]
+        n = len(b)
+        xs = np.empty((n, 4 * side))
+        ys = np.empty((n, 4 * side))
+        xs[:, 0:side], ys[:, 0:side] = left, top - k * dy
+        xs[:, side:2 * side], ys[:, side:2 * side] = left + k * dx, bottom
+        xs[:, 2 * side:3 * side], ys[:, 2 * side:3 * side] = right, bottom + k * dy
+        xs[:, 3 * side:], ys[:, 3 * side:] = right - k * dx, top
+        tx, ty = self.transform(xs.ravel(), ys.ravel())
+        tx, ty = tx.reshape(n, -1), ty.reshape(n, -1)
+        ok = np.isfinite(tx) & np.isfinite(ty)
+        out = np.stack([np.where(ok, tx, np.inf).min(axis=1), np.where(ok, ty, np.inf).min(axis=1),
+                        np.where(ok, tx, -np.inf).max(axis=1),
+                        np.where(ok, ty, -np.inf).max(axis=1)], axis=1)
+        out[~ok.any(axis=1)] = np.inf
+        return out

@@ -237,15 +237,33 @@ def plan_reproject(source_gm: GridMapping, target_gm: GridMapping,
 
     origin = source_gm.x_coords.values[0], source_gm.y_coords.values[0]
     bboxes = np.full((4, num_tiles_y, num_tiles_x), -1, dtype=np.int32)
-    for idx, xy_bbox in enumerate(target_gm.xy_bboxes):
-        j, i = np.unravel_index(idx, (num_tiles_y, num_tiles_x))
-        sb = transformer.transform_bounds(*xy_bbox)
-        bboxes[:, j, i] = [
-            math.floor((sb[0] - origin[0]) / source_gm.x_res),
-            math.floor((origin[1] - sb[3]) / source_gm.y_res),
-            math.ceil((sb[2] - origin[0]) / source_gm.x_res),
-            math.ceil((origin[1] - sb[1]) / source_gm.y_res),
-        ]
+    # all tiles' source bounds in one vectorised transform_bounds (the same
+    # values as tile by tile); a tile whose bounds are not finite takes the
+    # per-tile loop, which raises as the reference's math.floor does
+    sbs = transformer.transform_bounds_many(np.asarray(target_gm.xy_bboxes, dtype=np.float64))
+    edges = None
+    if np.isfinite(sbs).all():
+        sb0, sb1, sb2, sb3 = sbs.T
+        edges = np.stack([
+            np.floor((sb0 - origin[0]) / source_gm.x_res),
+            np.floor((origin[1] - sb3) / source_gm.y_res),
+            np.ceil((sb2 - origin[0]) / source_gm.x_res),
+            np.ceil((origin[1] - sb1) / source_gm.y_res),
+        ]).reshape(4, num_tiles_y, num_tiles_x)
+        if (np.abs(edges) > np.iinfo(np.int32).max).any():
+            edges = None   # the per-tile assignment raises OverflowError
+    if edges is not None:
+        bboxes[:] = edges
+    else:
+        for idx, xy_bbox in enumerate(target_gm.xy_bboxes):
+            j, i = np.unravel_index(idx, (num_tiles_y, num_tiles_x))
+            sb = transformer.transform_bounds(*xy_bbox)
+            bboxes[:, j, i] = [
+                math.floor((sb[0] - origin[0]) / source_gm.x_res),
+                math.floor((origin[1] - sb[3]) / source_gm.y_res),
+                math.ceil((sb[2] - origin[0]) / source_gm.x_res),
+                math.ceil((origin[1] - sb[1]) / source_gm.y_res),
+            ]
 
     # uniform window size (reproject.py:405-423)
     i_diff = bboxes[2] - bboxes[0]
