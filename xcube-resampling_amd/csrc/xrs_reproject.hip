@@ -53,13 +53,15 @@ constexpr int kRows = 8;                     // target rows whose loads are in f
 
 // K1b's work shape per output width.  float32 out: 512 columns x 32 rows,
 // 8 rows in flight.  float64 out (the reference's bilinear dtype, twice the
-// store bytes): 1024 columns x 8 rows, 4 rows in flight — 6 % faster there
-// and 2 % slower for float32 (A/B interleaved on one box,
-// profiles/r03_k1_shapes_ab.jsonl), so each output width takes its own.
+// store bytes): 1024 columns x 12 rows, 4 rows in flight — with the round-5
+// prologue 2 % faster than the 8-row bands of rounds 3-4 (3.533 vs 3.603-3.615
+// ms at config 5, profiles/r05_k1_f64out_shapes_ab.jsonl; 512 x 16 3.56,
+// 1024 x 16 3.58, 512 x 32 3.60); each output width takes its own shape
+// (profiles/r03_k1_shapes_ab.jsonl).
 template <typename O>
 struct K1Shape {
   static constexpr int px = sizeof(O) == 8 ? 4 : kPx;
-  static constexpr int band = sizeof(O) == 8 ? 8 : kBand;
+  static constexpr int band = sizeof(O) == 8 ? 12 : kBand;
   static constexpr int rows = sizeof(O) == 8 ? 4 : kRows;
   static constexpr int segw = kThreads * px;
 };
