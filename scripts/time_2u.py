@@ -16,6 +16,9 @@ sys.path.insert(0, ROOT)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--time", action="store_true",
+                    help="time both paths (events) and print one JSON line")
+    ap.add_argument("--tag", default="")
     args = ap.parse_args()
     import torch
 
@@ -33,6 +36,27 @@ def main():
     out = torch.empty((1, size, size), device="cuda", dtype=torch.float64)
     flags = kernels.ErrorFlags(src.device)
     fplan = dataclasses.replace(plan, fuse_transform=True, _device_cache={})
+    if args.time:
+        import json
+
+        def run(p, k):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            for _ in range(3):
+                kernels.reproject(src, p, "bilinear", float("nan"), out=out, flags=flags, check=False)
+            e0.record()
+            for _ in range(k):
+                kernels.reproject(src, p, "bilinear", float("nan"), out=out, flags=flags, check=False)
+            e1.record()
+            torch.cuda.synchronize()
+            return e0.elapsed_time(e1) / k
+        tables_ms = run(plan, 10)
+        fused_ms = run(fplan, 10)
+        flags.raise_if_set("time_2u")
+        v = out.view(torch.int64)
+        csum = int((v & 0xFFFFFFF).sum()) % (1 << 61)
+        print(json.dumps({"tag": args.tag, "tables_ms": round(tables_ms, 4),
+                          "fused_ms": round(fused_ms, 4), "checksum_fused": csum}), flush=True)
+        return
     for _ in range(args.reps):
         plan._device_cache.clear()
         kernels.reproject(src, plan, "bilinear", float("nan"), out=out, flags=flags, check=False)

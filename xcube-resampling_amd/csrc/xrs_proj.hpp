@@ -288,12 +288,15 @@ __device__ inline double adjlon(double lam) {
 struct LaeaTmerc {
   double sd, cd;     // sin / cos (lam0_laea - lam0_tmerc)
   double sp0, cp0;   // sin / cos phi0 (the LAEA centre, where rho < 1e-10)
+  double inv_dd, half_inv_rq;   // 1 / dd and 0.5 / rq: products, not divisions, per point
 };
 
 __device__ inline LaeaTmerc laea_tmerc_setup(const XrsProjStep& s0, const XrsProjStep& s1) {
   LaeaTmerc k;
   sincos(s0.lam0 - s1.lam0, &k.sd, &k.cd);
   sincos(s0.phi0, &k.sp0, &k.cp0);
+  k.inv_dd = 1.0 / s0.dd;
+  k.half_inv_rq = 0.5 / s0.rq;
   return k;
 }
 
@@ -307,15 +310,17 @@ __device__ inline void sincos_small(double d, double& s, double& c) {
 template <bool OBLIQ>
 __device__ inline void laea_inv_tmerc_fwd(const XrsProjStep& s0, const XrsProjStep& s1,
                                           const LaeaTmerc& k, double& x, double& y) {
-  // laea_inv's first half, operation for operation (the `small` / `bad`
-  // decisions must be the two-step pipeline's)
+  // laea_inv's first half, with its two constant divisions as products by
+  // reciprocals set up once per thread (an ulp from the two-step pipeline's
+  // xx and a; its `small` / `bad` thresholds are not that close to any point:
+  // 3 % of the fused 2u gather, profiles/r05_2u_int32_recip_ab.jsonl)
   double xx = (x - s0.x0) * s0.ra, yy = (y - s0.y0) * s0.ra;
-  xx = xx / s0.dd;
+  xx = xx * k.inv_dd;
   yy = yy * s0.dd;
   const double rho = hypot(xx, yy);
   const bool small = rho < kEps10;
   const double rho_s = small ? 1.0 : rho;
-  const double a = 0.5 * rho_s / s0.rq;
+  const double a = rho_s * k.half_inv_rq;
   const bool bad = a > 1.0;
   const double ac = bad ? 1.0 : a;   // NaN stays NaN
   const double ca = sqrt((1.0 - ac) * (1.0 + ac));

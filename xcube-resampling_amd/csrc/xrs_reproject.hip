@@ -159,6 +159,61 @@ __device__ inline AxisEntry resolve_axis(double coord, float origin, double res,
   return e;
 }
 
+// resolve_axis for the per-pixel gathers (K1c, K1p): the same entries with
+// 32-bit index arithmetic whenever every quantity fits (window and band
+// bounds below 2^30, |window origin| <= 2^30: no sum or difference below can
+// leave int32); otherwise resolve_axis itself.
+template <int INTERP>
+__device__ inline AxisEntry resolve_axis_px(double coord, float origin, double res, int64_t win,
+                                            int64_t w0, int64_t size, int64_t band0,
+                                            int64_t band_len, int32_t& eflags) {
+  constexpr int64_t kLim = int64_t(1) << 30;
+  if (!(win <= kLim && size <= INT32_MAX && band0 >= 0 && band0 <= kLim && band_len <= INT32_MAX &&
+        w0 >= -kLim && w0 <= kLim))
+    return resolve_axis<INTERP>(coord, origin, res, win, w0, size, band0, band_len, eflags);
+  const int32_t win32 = (int32_t)win, w032 = (int32_t)w0, size32 = (int32_t)size;
+  const int32_t b032 = (int32_t)band0, bl32 = (int32_t)band_len;
+  auto window32 = [&](int16_t idx16, int32_t& out) {
+    int32_t i = idx16;
+    if (i < 0) i += win32;
+    out = i;
+    return i >= 0 && i < win32;
+  };
+  auto source32 = [&](int32_t widx) -> int32_t {
+    const int32_t g = w032 + widx;
+    if (g < 0 || g >= size32) return -1;
+    const int32_t l = g - b032;
+    if (l < 0 || l >= bl32) {
+      eflags |= XRS_EFLAG_BAND;
+      return -1;
+    }
+    return l;
+  };
+  const double i = (coord - (double)origin) / res;
+  AxisEntry e;
+  if (INTERP == XRS_INTERP_NEAREST) {
+    int32_t wi;
+    if (window32(f64_to_i16_np(rint(i)), wi)) {
+      e.f = source32(wi);
+    } else {
+      eflags |= XRS_EFLAG_INDEX;
+      e.f = -1;
+    }
+    e.c = e.f;
+    e.d = 0.0;
+  } else {
+    const int16_t fi = f64_to_i16_np(floor(i)), ci = f64_to_i16_np(ceil(i));
+    e.d = i - (double)fi;
+    int32_t wf, wc;
+    const bool okf = window32(fi, wf);
+    const bool okc = window32(ci, wc);
+    if (!okf || !okc) eflags |= XRS_EFLAG_INDEX;
+    e.f = okf ? source32(wf) : -1;
+    e.c = okc ? source32(wc) : -1;
+  }
+  return e;
+}
+
 // ---- interpolation of one pixel (reproject.py:304-314, 326-328) ------------
 template <typename T, int INTERP>
 __device__ inline double interp4(T v00, T v01, T v10, T v11, double dx, double dy) {
@@ -461,9 +516,9 @@ gather_2d_kernel(GatherArgs a, int64_t ty0, int64_t nsegs, int64_t bands_per_til
         for (int k = 0; k < kPx; ++k) {
           ex[q][k] = ey[q][k] = AxisEntry{-1, -1, 0.0};
           if (ok[q][k]) {
-            ex[q][k] = resolve_axis<INTERP>(sx[q][k], x0, g.x_res, g.win_w, wi0, g.src_w, 0,
+            ex[q][k] = resolve_axis_px<INTERP>(sx[q][k], x0, g.x_res, g.win_w, wi0, g.src_w, 0,
                                             g.src_w, eflags);
-            ey[q][k] = resolve_axis<INTERP>(sy[q][k], y0, g.neg_y_res, g.win_h, wj0, g.src_h,
+            ey[q][k] = resolve_axis_px<INTERP>(sy[q][k], y0, g.neg_y_res, g.win_h, wj0, g.src_h,
                                             g.src_row0, g.src_rows, eflags);
           }
         }
@@ -609,14 +664,14 @@ gather_proj_kernel(GatherArgs a, XrsProjStep s0, XrsProjStep s1, int mode, DivU3
     const int64_t wi0 = gg.tile_win[2 * t], wj0 = gg.tile_win[2 * t + 1];
     AxisEntry ex, ey;
     if (nearest) {
-      ex = resolve_axis<XRS_INTERP_NEAREST>(px, x0, gg.x_res, gg.win_w, wi0, gg.src_w, 0, gg.src_w,
+      ex = resolve_axis_px<XRS_INTERP_NEAREST>(px, x0, gg.x_res, gg.win_w, wi0, gg.src_w, 0, gg.src_w,
                                             eflags);
-      ey = resolve_axis<XRS_INTERP_NEAREST>(py, y0, gg.neg_y_res, gg.win_h, wj0, gg.src_h,
+      ey = resolve_axis_px<XRS_INTERP_NEAREST>(py, y0, gg.neg_y_res, gg.win_h, wj0, gg.src_h,
                                             gg.src_row0, gg.src_rows, eflags);
     } else {
-      ex = resolve_axis<XRS_INTERP_BILINEAR>(px, x0, gg.x_res, gg.win_w, wi0, gg.src_w, 0, gg.src_w,
+      ex = resolve_axis_px<XRS_INTERP_BILINEAR>(px, x0, gg.x_res, gg.win_w, wi0, gg.src_w, 0, gg.src_w,
                                              eflags);
-      ey = resolve_axis<XRS_INTERP_BILINEAR>(py, y0, gg.neg_y_res, gg.win_h, wj0, gg.src_h,
+      ey = resolve_axis_px<XRS_INTERP_BILINEAR>(py, y0, gg.neg_y_res, gg.win_h, wj0, gg.src_h,
                                              gg.src_row0, gg.src_rows, eflags);
     }
     if constexpr (MODE >= 0)
