@@ -316,15 +316,21 @@ template <bool OBLIQ>
 __device__ inline void laea_inv_tmerc_fwd(const XrsProjStep& s0, const XrsProjStep& s1,
                                           const LaeaTmerc& k, double& x, double& y) {
   // laea_inv's first half, with its two constant divisions as products by
-  // reciprocals set up once per thread (an ulp from the two-step pipeline's
-  // xx and a; its `small` / `bad` thresholds are not that close to any point:
-  // 3 % of the fused 2u gather, profiles/r05_2u_int32_recip_ab.jsonl)
+  // reciprocals set up once per thread and the radius from sqrt / rsqrt of
+  // one sum of squares (each an ulp from the two-step pipeline's xx, rho and
+  // a; its `small` / `bad` thresholds are not that close to any point: 3 % and
+  // 1-2 % of the fused 2u gather, profiles/r05_2u_int32_recip_ab.jsonl,
+  // r05_2u_rho_rsqrt_ab.jsonl)
   double xx = (x - s0.x0) * s0.ra, yy = (y - s0.y0) * s0.ra;
   xx = xx * k.inv_dd;
   yy = yy * s0.dd;
-  const double rho = hypot(xx, yy);
+  // |xx|, |yy| are a few earth radii at most: no scaling needed; rho and
+  // its reciprocal from one sum of squares (an ulp from hypot / a division)
+  const double r2s = xx * xx + yy * yy;
+  const double rho = sqrt(r2s);
   const bool small = rho < kEps10;
   const double rho_s = small ? 1.0 : rho;
+  const double inv_rho_s = small ? 1.0 : rsqrt(r2s);
   const double a = rho_s * k.half_inv_rq;
   const bool bad = a > 1.0;
   const double ac = bad ? 1.0 : a;   // NaN stays NaN
@@ -334,10 +340,10 @@ __device__ inline void laea_inv_tmerc_fwd(const XrsProjStep& s0, const XrsProjSt
   const double X = xx * sCe;
   double ab, Y;
   if constexpr (OBLIQ) {
-    ab = cCe * s0.sinb1 + yy * sCe * s0.cosb1 / rho_s;
+    ab = cCe * s0.sinb1 + yy * sCe * s0.cosb1 * inv_rho_s;
     Y = rho_s * s0.cosb1 * cCe - yy * s0.sinb1 * sCe;
   } else {
-    ab = yy * sCe / rho_s;
+    ab = yy * sCe * inv_rho_s;
     Y = rho_s * cCe;
   }
   // longitude atan2(X, Y) (0 at the centre), shifted to tmerc's central meridian
