@@ -125,8 +125,10 @@ __device__ inline void tmerc_fwd_tail(const XrsProjStep& s, double sin_Cn, doubl
   const double tan_Ce = sin_Ce * cos_Cn * inv_denom_tan_Ce;
   // asinh through log (|tan_Ce| < 7 here: no overflow guard needed; absolute
   // error ~1e-16, i.e. ~1e-9 m, where the library's asinh keeps relative
-  // precision near 0 at 1.6x the instructions)
-  double Ce = copysign(log_ge1(fabs(tan_Ce) + sqrt(tan_Ce * tan_Ce + 1.0)), tan_Ce);
+  // precision near 0 at 1.6x the instructions).  sqrt(tan_Ce^2 + 1) is
+  // 1 / |(sin_Cn, cos_Cn cos_Ce)| = inv_denom_tan_Ce (sin^2 + cos^2 = 1 for
+  // both pairs, to an ulp): no square root
+  double Ce = copysign(log_ge1(fabs(tan_Ce) + inv_denom_tan_Ce), tan_Ce);
   const double two_inv_denom_tan_Ce = 2 * inv_denom_tan_Ce;
   const double two_inv_denom_tan_Ce_square = two_inv_denom_tan_Ce * inv_denom_tan_Ce;
   const double tmp_r = cos_Cn_cos_Ce * two_inv_denom_tan_Ce_square;
