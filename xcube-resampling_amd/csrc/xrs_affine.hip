@@ -124,7 +124,7 @@ affine_tables_kernel(AxisChunks ay, AxisChunks ax, AxisTab* __restrict__ ytab,
                      AxisTab* __restrict__ xtab, int64_t dy, int64_t dx,
                      int32_t* __restrict__ counters, const int64_t* __restrict__ t_next,
                      int64_t nt, bool check_self, int32_t* __restrict__ yrun,
-                     int32_t* __restrict__ xrun) {
+                     int32_t* __restrict__ xrun, bool wave_runs) {
   if (counters && blockIdx.x == 0) {
     bool other = false;   // K3i: a zero-weight time neighbour other than the slice?
     if (check_self)
@@ -144,7 +144,17 @@ affine_tables_kernel(AxisChunks ay, AxisChunks ax, AxisTab* __restrict__ ytab,
     const AxisTab e = axis_entry<ORDER>(ac, o);
     (is_y ? ytab : xtab)[o] = e;
     const int64_t d = is_y ? dy : dx;
-    if (counters && o % d == 0) {   // K3i's run record of output row / column o / d
+    if (wave_runs) {
+      // a run's d entries sit on consecutive lanes of one wave (d divides 64,
+      // runs start at multiples of d on both axes: checked at launch): each
+      // lane tests its own entry against the run's first, a ballot ANDs them
+      const int lane = (int)(threadIdx.x & 63);
+      const int k = (int)(o % d);
+      const int32_t g_first = __shfl(e.g0, lane - k);
+      const uint64_t bad = __ballot(!integral_entry<ORDER>(e, g_first, k));
+      if (k == 0)
+        (is_y ? yrun : xrun)[o / d] = ((bad >> lane) & ((1ull << d) - 1)) == 0 ? e.g0 : -1;
+    } else if (counters && o % d == 0) {   // K3i's run record of row / column o / d
       bool ok = e.g0 >= 0 && integral_entry<ORDER>(e, e.g0, 0);
       for (int64_t j = 1; j < d && ok; ++j)
         ok = integral_entry<ORDER>(axis_entry<ORDER>(ac, o + j), e.g0, (int)j);
@@ -1004,9 +1014,12 @@ int launch(const AffineArgs& a, const AxisChunks& ay, const AxisChunks& ax, Axis
   // K3i's run records (one int32 per output row / column) after the slow list
   int32_t* yrun = reinterpret_cast<int32_t*>(slow_list + slow_cap);
   int32_t* xrun = yrun + a.out_h;
+  // run records by a wave ballot when every run sits inside one wave
+  const bool wave_runs = k3i && a.dy > 0 && a.dx > 0 && 64 % a.dy == 0 && 64 % a.dx == 0 &&
+                         ay.n % a.dy == 0 && ay.n % a.dx == 0 && ax.n % a.dx == 0;
   hipLaunchKernelGGL((affine_tables_kernel<ORDER>), dim3(nbt), dim3(kThreads), 0, st, ay, ax,
                      ytab, xtab, a.dy, a.dx, k3i ? nonint : nullptr, a.t_next, a.nt,
-                     t1_flag, yrun, xrun);
+                     t1_flag, yrun, xrun, wave_runs);
   XRS_HIP_CHECK(hipGetLastError());
   if (k3i) {
     const int64_t ntiles = ((a.out_w + kThreads - 1) / kThreads) *
