@@ -78,15 +78,15 @@ const char* xrs_last_error(void);
  * page boundary and `bytes` a multiple of the page size (else XRS_ERR_ARG —
  * a malloc'd numpy array shares its edge pages with its neighbours); returns
  * XRS_OK, 1 when the range was already registered (the caller must then NOT
- * unregister it), or XRS_ERR_HIP.  xrs_host_unregister drains every visible
- * device (every stream) before unpinning, so no queued copy outlives the
- * pinning; the calling thread's current device is restored.  It stalls work
- * unrelated to the range, and must not run while another thread captures a
- * graph: bindings that know which streams used the range may synchronise
- * those instead and unregister outside capture windows.
+ * unregister it), or XRS_ERR_HIP.  xrs_host_unregister synchronises the
+ * `nstreams` (1..64) streams the caller names — every stream that copied
+ * to or from the range (a null entry is the current device's null stream)
+ * — then unpins; no other stream or device waits, so one host thread per
+ * device may unregister while the others keep their queues busy.  A stream
+ * still queueing copies of the range after the call is the caller's error.
  * ------------------------------------------------------------------------- */
 int xrs_host_register(void* ptr, int64_t bytes);
-int xrs_host_unregister(void* ptr);
+int xrs_host_unregister(void* ptr, void* const* streams, int64_t nstreams);
 /* stream-ordered copy of `bytes` between any two of host / device memory
  * (hipMemcpyAsync, direction from unified addressing) */
 int xrs_copy_async(void* dst, const void* src, int64_t bytes, void* stream);
@@ -360,6 +360,9 @@ int xrs_rectify_var(const double* ij, int64_t ij_sn, int64_t dst_h, int64_t dst_
  *   XRS_TESTING_RECTIFY_PLAIN_KEYS        1: K5 claims with plain raster keys and
  *                                         the resolve tests both triangles (the
  *                                         path of swaths of 2^31 points or more)
+ *   XRS_TESTING_PROJ_TWO_STEP             1: LAEA inverse -> tmerc forward runs as
+ *                                         two library-transcendental steps instead
+ *                                         of the fused sine / cosine pipeline
  * Returns the previous value (or XRS_ERR_ARG for an unknown knob).
  * ------------------------------------------------------------------------- */
 #define XRS_TESTING_REPROJECT_BAND 1
@@ -368,7 +371,8 @@ int xrs_rectify_var(const double* ij, int64_t ij_sn, int64_t dst_h, int64_t dst_
 #define XRS_TESTING_RECTIFY_EXACT 4
 #define XRS_TESTING_RECTIFY_MARGIN 5
 #define XRS_TESTING_RECTIFY_PLAIN_KEYS 7
-#define XRS_TESTING_NUM_KNOBS 8
+#define XRS_TESTING_PROJ_TWO_STEP 8
+#define XRS_TESTING_NUM_KNOBS 9
 int64_t xrs_testing_set(int knob, int64_t value);
 
 /* ---- coordinate transformation (reproject.py:472-496, rectify.py:182-231) --

@@ -178,6 +178,40 @@ def issue_pmc(kernels=("claim", "resolve", "ij_bboxes"), timeout=150,
         shutil.rmtree(d, ignore_errors=True)
 
 
+def kernel_times(interp, timeout=150, reps=30):
+    """The fused config-4 pipeline's own kernels (scripts/time_rectify.py
+    --fused: K4 + device tiling + claim + resolve with K6 inside), average
+    microseconds per launch from one rocprofv3 --kernel-trace --stats child
+    run; None when rocprofv3 is absent or fails."""
+    import csv
+    import shutil
+    import subprocess
+    import tempfile
+
+    prof = shutil.which("rocprofv3")
+    if prof is None:
+        return None
+    d = tempfile.mkdtemp(prefix="xrs_kt_", dir=os.environ.get("TMPDIR", "/tmp"))
+    cmd = ["timeout", "-s", "KILL", str(timeout), prof, "--kernel-trace", "--stats",
+           "--output-format", "csv", "-d", d, "-o", "kt", "--", sys.executable,
+           os.path.join(ROOT, "scripts", "time_rectify.py"), "--fused", "--interp", interp,
+           "--reps", str(reps)]
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        print(f"kernel_times: rocprofv3 failed (rc {r.returncode}):\n{r.stdout[-1500:]}",
+              file=sys.stderr)
+        return None
+    names = {"K4 ij_bboxes": "ij_bboxes", "tiles": "rectify_tiles_kernel",
+             "K5a claim": "rectify_claim_kernel", "K5b resolve + K6 (fused)": "rectify_resolve_kernel"}
+    out = {}
+    for path in _find(d, "kernel_stats.csv"):
+        for row in csv.DictReader(open(path)):
+            for label, key in names.items():
+                if key in row["Name"]:
+                    out[label] = out.get(label, 0.0) + float(row["AverageNs"]) / 1e3
+    return {k: round(v, 1) for k, v in out.items()} or None
+
+
 def _find(root, suffix):
     for dp, _, files in os.walk(root):
         for f in files:
@@ -506,18 +540,22 @@ def config4(args):
             best = min(best, time.perf_counter() - t0)
             del ij_c
         cpu_v, dt = npx / best / 1e6, best
+        kt = kernel_times(interp)
+        kern = ("fused pipeline: " + ", ".join(f"{k} {v:.1f} us" for k, v in kt.items()) +
+                f" (sum {sum(kt.values()) / 1e3:.3f} ms)") if kt else "fused pipeline"
         _line(4, f"rectify {interp}: 4000x4800 jittered swath (f64 lon/lat, f32 var) -> "
                  f"{tgm.width}x{tgm.height} EPSG:4326 res 0.0027, 512^2 tiles "
                  "(K4 bbox + device tiling + K5 with K6 fused, end to end, coordinates "
                  "resident in HBM)",
               npx, ms, wall, 16 * S + 4 * S + 4 * npx,
-              f"K5 rectify_claim+resolve {k5_ms:.3f} ms, K6 {lines[interp]:.3f} ms",
+              kern,
               dict(value=round(cpu_v, 2), unit="Mpixels/s", cores=cores, kind="port",
                    sample=f"the whole config: 4000x4800 swath -> {tgm.width}x{tgm.height}, "
                           f"C restatement of the numba kernels (bboxes, ij, var image; tiles "
                           f"on a {cores}-thread pool), best of 3 passes: {dt:.2f} s"),
-              {"covered_px": covered, "k5_ms": round(k5_ms, 4),
-               "k6_ms": round(lines[interp], 4), "unfused_ms": round(sep_ms, 4),
+              {"covered_px": covered, "kernels_us": kt,
+               "unfused": {"k5_claim_resolve_ms": round(k5_ms, 4),
+                           "k6_ms": round(lines[interp], 4), "pipeline_ms": round(sep_ms, 4)},
                "issue": issue})
     flags.raise_if_set("config 4")
 

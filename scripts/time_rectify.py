@@ -2,7 +2,7 @@
 resolve, K6 nearest): the workload of scripts/bench_configs.py config4, for
 rocprofv3 --kernel-trace --stats runs of kernel variants.  --fused samples the
 variable inside K5's resolve pass (xrs_rectify_ij_var, no ij image written).
-    python scripts/time_rectify.py [--reps N] [--fused]"""
+    python scripts/time_rectify.py [--reps N] [--fused] [--interp nearest|bilinear|triangular]"""
 
 from __future__ import annotations
 
@@ -21,6 +21,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--fused", action="store_true")
+    ap.add_argument("--interp", default="nearest", choices=["nearest", "bilinear", "triangular"])
     args = ap.parse_args()
     import torch
 
@@ -54,12 +55,12 @@ def main():
         t = R._device_tiles(sgm, tgm, xy)
         if args.fused:
             _, out = kernels.rectify_ij_var(xy[0], xy[1], t, tgm.height, tgm.width, tgm.x_res,
-                                            -tgm.y_res, 1e-3, src, "nearest", float("nan"),
+                                            -tgm.y_res, 1e-3, src, args.interp, float("nan"),
                                             keep_ij=False, flags=flags)
         else:
             ij = kernels.rectify_ij(xy[0], xy[1], t, ntx, tgm.height, tgm.width, tgm.x_res,
                                     -tgm.y_res, 1e-3, flags=flags)
-            out = kernels.rectify_var(ij, src, "nearest", float("nan"), flags=flags)
+            out = kernels.rectify_var(ij, src, args.interp, float("nan"), flags=flags)
     ev[1].record()
     torch.cuda.synchronize()
     flags.raise_if_set("time_rectify")

@@ -40,6 +40,14 @@ def test_devices_option_and_keyword_scope():
         with multidevice.use_devices(["cuda:3"]):   # the keyword wins over the option
             assert multidevice.active_devices() == [torch.device("cuda", 3)]
         assert len(multidevice.active_devices()) == 3
+    # an index-less "cuda" is the current device when normalised
+    monkey = pytest.MonkeyPatch()
+    monkey.setattr(torch.cuda, "current_device", lambda: 5)
+    try:
+        assert multidevice.normalize(["cuda", 2]) == [torch.device("cuda", 5),
+                                                      torch.device("cuda", 2)]
+    finally:
+        monkey.undo()
     for bad in ([], [-1], ["cpu"], "cuda:0", [True], [1.5]):
         with pytest.raises(ValueError):
             with xrs.set_options(devices=bad):

@@ -272,3 +272,25 @@ def test_devices_more_parts_than_rows():
     out = xrs.rectify_dataset(dataset_2x2_irregular(), target_gm=rtgm, interp_methods=0,
                               devices=[0] * 12)
     np.testing.assert_almost_equal(out["rad"].values, gold)
+
+
+def test_affine_workspaces_bounded_per_stream():
+    """K2/K3 workspaces are keyed by (device, stream) and the cache keeps at
+    most _WORKSPACES_MAX of them (one per pool stream, forever):
+    twelve streams leave eight entries, the most recent ones, and a stream's
+    entry is reused while it stays cached."""
+    import torch
+
+    from xcube_resampling_amd import kernels
+
+    dev = torch.device("cuda", 0)
+    streams = [torch.cuda.Stream(device=dev) for _ in range(12)]
+    for s in streams:
+        kernels._workspace(dev, 1 << 16, s)
+    keys = [(str(dev), int(s.cuda_stream)) for s in streams]
+    assert len(kernels._WORKSPACES) <= kernels._WORKSPACES_MAX
+    assert all(k in kernels._WORKSPACES for k in keys[-kernels._WORKSPACES_MAX:])
+    assert not any(k in kernels._WORKSPACES for k in keys[:12 - kernels._WORKSPACES_MAX])
+    ws = kernels._workspace(dev, 1 << 10, streams[-1])
+    assert ws is kernels._workspace(dev, 1 << 12, streams[-1])   # cached, large enough
+    torch.cuda.synchronize()

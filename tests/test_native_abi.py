@@ -144,7 +144,12 @@ def test_host_register_refuses_partial_pages():
             assert lib.xrs_host_register(ctypes.c_void_p(ptr), size) == _native.XRS_ERR_ARG
             assert "page" in _native.last_error()
         assert lib.xrs_host_register(None, page) == _native.XRS_ERR_ARG
-        assert lib.xrs_host_unregister(None) == _native.XRS_ERR_ARG
+        one = (ctypes.c_void_p * 1)(None)
+        assert lib.xrs_host_unregister(None, one, 1) == _native.XRS_ERR_ARG
+        # the caller must name the streams that used the range (no device drain)
+        assert lib.xrs_host_unregister(ctypes.c_void_p(base), None, 1) == _native.XRS_ERR_ARG
+        assert lib.xrs_host_unregister(ctypes.c_void_p(base), one, 0) == _native.XRS_ERR_ARG
+        assert lib.xrs_host_unregister(ctypes.c_void_p(base), one, 65) == _native.XRS_ERR_ARG
     finally:
         del base
         buf.close()

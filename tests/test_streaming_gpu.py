@@ -311,7 +311,9 @@ def test_host_register_copy_unregister_then_fresh_pageable_copy():
         _native.check(lib.xrs_copy_async(ctypes.c_void_p(dev.data_ptr()), ctypes.c_void_p(ptr),
                                          nbytes, ctypes.c_void_p(stream.cuda_stream)),
                       "xrs_copy_async")
-        _native.check(lib.xrs_host_unregister(ctypes.c_void_p(ptr)), "xrs_host_unregister")
+        streams = (ctypes.c_void_p * 1)(stream.cuda_stream)   # the stream that copied
+        _native.check(lib.xrs_host_unregister(ctypes.c_void_p(ptr), streams, 1),
+                      "xrs_host_unregister")
         expect = host.copy()
         assert_bitwise_equal(dev.cpu().numpy(), expect, f"registered copy {k}")
         del host

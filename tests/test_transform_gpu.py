@@ -327,3 +327,72 @@ def test_reproject_dataset_fuses_when_tables_exceed_budget():
         g = g.cpu().numpy() if hasattr(g, "cpu") else g
         assert np.isfinite(r).mean() > 0.5
         assert np.array_equal(r, g, equal_nan=True)
+
+
+@pytest.mark.parametrize("lat_0", [52.0, 0.0])   # oblique (EPSG:3035's aspect), equatorial
+def test_fused_laea_tmerc_decisions_at_thresholds(lat_0):
+    """The fused LAEA -> tmerc pipeline takes laea_inv's `bad` (a = rho / 2rq
+    > 1: outside the disk, non-finite) and `small` (rho < 1e-10: the centre)
+    decisions exactly as the two-step pipeline does: on rays
+    from the centre the two-step pipeline's own thresholds are found by
+    bisection, and a 21 x 21 grid of points ulp by ulp around each crossing
+    gives the same non-finite mask on both paths (test knob
+    XRS_TESTING_PROJ_TWO_STEP), and values within the module's tolerance
+    around the centre."""
+    import xcube_resampling_amd as xrs
+    from xcube_resampling_amd import _native, kernels
+
+    x0, y0 = 1.0e6, 5.0e5
+    laea = xrs.CRS.from_cf({"grid_mapping_name": "lambert_azimuthal_equal_area",
+                            "latitude_of_projection_origin": lat_0,
+                            "longitude_of_projection_origin": 9.0,
+                            "false_easting": x0, "false_northing": y0,
+                            "inverse_flattening": 298.257223563})
+    # the small threshold is at the centre (9 E: UTM zone 32), the bad one on
+    # the disk's edge, which maps to the antipode (171 W: UTM zone 2, where
+    # tmerc is well conditioned and decides nothing of its own)
+    trs = {"small": xrs.Transformer.from_crs(laea, "EPSG:32632", always_xy=True),
+           "bad": xrs.Transformer.from_crs(laea, "EPSG:32702", always_xy=True)}
+
+    def run(what, x, y, two_step):
+        with _native.testing_knob("proj_two_step", 1 if two_step else 0):
+            ox, oy = kernels.transform(trs[what], np.atleast_2d(x), np.atleast_2d(y), False)
+        return ox.cpu().numpy().ravel(), oy.cpu().numpy().ravel()
+
+    th = np.linspace(0.0, 2 * np.pi, 48, endpoint=False) + 0.01
+    c, s = np.cos(th), np.sin(th)
+    cx, cy = run("small", np.array([x0]), np.array([y0]), True)
+
+    def bisect(what, lo, hi, is_hi):   # per ray: lo on one side, hi on the other
+        lo, hi = np.full(th.size, lo), np.full(th.size, hi)
+        for _ in range(80):
+            mid = 0.5 * (lo + hi)
+            h = is_hi(*run(what, x0 + mid * c, y0 + mid * s, True))
+            lo, hi = np.where(h, lo, mid), np.where(h, mid, hi)
+        return hi
+
+    d_bad = bisect("bad", 0.0, 4.0e7, lambda ox, oy: ~np.isfinite(ox))
+    d_small = bisect("small", 1.0, 0.0, lambda ox, oy: (ox == cx[0]) & (oy == cy[0]))
+    assert (d_small > 1e-4).all() and (d_small < 1e-2).all()   # rho = 1e-10 earth radii
+    assert (d_bad > 1.2e7).all() and (d_bad < 1.3e7).all()     # rho = 2 rq
+    k = np.arange(-10, 11)
+    for d, what in ((d_bad, "bad"), (d_small, "small")):
+        px, py = x0 + d * c, y0 + d * s
+        gx = np.concatenate([px[i] + k * np.spacing(px[i]) for i in range(th.size)])
+        gy = np.concatenate([py[i] + k * np.spacing(py[i]) for i in range(th.size)])
+        xx = (gx.reshape(th.size, 1, -1) + 0 * gy.reshape(th.size, -1, 1)).ravel()
+        yy = (gy.reshape(th.size, -1, 1) + 0 * gx.reshape(th.size, 1, -1)).ravel()
+        fx, fy = run(what, xx, yy, False)
+        tx, ty = run(what, xx, yy, True)
+        fin = np.isfinite(tx)
+        np.testing.assert_array_equal(np.isfinite(fx), fin, err_msg=what)
+        np.testing.assert_array_equal(np.isfinite(fy), np.isfinite(ty), err_msg=what)
+        if what == "bad":
+            # the sample straddles the threshold; values are not compared here:
+            # at the disk's edge the inverse is singular (d Ce / d a = 2 /
+            # sqrt(1 - a^2)), so the paths' ulp-apart a give points up to
+            # ~0.3 m apart near the antipode
+            assert 0 < fin.sum() < fin.size
+            continue
+        np.testing.assert_allclose(fx[fin], tx[fin], rtol=RTOL, atol=ATOL["m"], err_msg=what)
+        np.testing.assert_allclose(fy[fin], ty[fin], rtol=RTOL, atol=ATOL["m"], err_msg=what)

@@ -88,7 +88,7 @@ _SIGNATURES = {
     "xrs_version": (ctypes.c_char_p, []),
     "xrs_last_error": (ctypes.c_char_p, []),
     "xrs_host_register": (_c_int, [_c_ptr, _c_i64]),
-    "xrs_host_unregister": (_c_int, [_c_ptr]),
+    "xrs_host_unregister": (_c_int, [_c_ptr, _c_ptr, _c_i64]),
     "xrs_copy_async": (_c_int, [_c_ptr, _c_ptr, _c_i64, _c_ptr]),
     "xrs_reproject": (_c_int, [
         _c_ptr, _c_int, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64,  # src
@@ -169,7 +169,7 @@ MAX_PROJ_STEPS = 4
 
 TESTING_KNOBS = {"reproject_band": 1, "reproject_blocks_per_cu": 2, "affine_generic": 3,
                  "rectify_exact": 4, "rectify_margin": 5,
-                 "rectify_plain_keys": 7}   # 6: retired (K1's column-group deal, round 5)
+                 "rectify_plain_keys": 7, "proj_two_step": 8}   # 6: retired (K1's column-group deal, round 5)
 
 
 class testing_knob:

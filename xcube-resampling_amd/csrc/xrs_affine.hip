@@ -877,7 +877,11 @@ affine_reduce_integral_kernel(AffineArgs a, const int32_t* __restrict__ yrun,
         });
       fold.store(a, didx);
     }
+    // once the list has overflowed the finish reruns the whole launch through
+    // the generic K3, so nothing K3i still does would be kept: stop (a grid
+    // off the integral layout overflows within every wave's first item)
     full = full || __any(overflow);
+    if (full) break;
   }
 }
 
@@ -959,8 +963,9 @@ inline int64_t reduce_row_bytes(int64_t dx, int64_t isize) {
 // tables really are integral is known on the device only (affine_tables_kernel
 // writes the run records), so K3i and its finish are launched; the finish runs
 // the slow pixels K3i listed, or the generic K3 over the whole launch when the
-// list overflowed (a grid off the integral layout: K3i then stops loading as
-// soon as the list is full).
+// list overflowed (a grid off the integral layout: every wave of K3i returns
+// at the first item in which it sees the list full, since the finish then
+// overwrites everything K3i would store).
 // xrs_testing_set(XRS_TESTING_AFFINE_GENERIC, 1) forces the generic K3 (tests).
 template <typename T, typename I, bool RECOVER>
 inline bool integral_candidate(const AffineArgs& a) {

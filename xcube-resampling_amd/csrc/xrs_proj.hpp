@@ -291,7 +291,8 @@ __device__ inline double adjlon(double lam) {
 // Ten f64 transcendentals per point (asin x2, sincos x5, atan2, ...) become
 // two square roots, two hypots and two divisions; results agree with the
 // two-step restatement to a few ulps (tests/test_transform_gpu.py tolerances),
-// non-finite in the same places (the same `bad` / `ok` decisions).
+// non-finite in the same places: the `small` / `bad` decisions are re-taken
+// in the two-step order wherever the fast values are near a threshold.
 struct LaeaTmerc {
   double sd, cd;     // sin / cos (lam0_laea - lam0_tmerc)
   double sp0, cp0;   // sin / cos phi0 (the LAEA centre, where rho < 1e-10)
@@ -319,23 +320,32 @@ __device__ inline void laea_inv_tmerc_fwd(const XrsProjStep& s0, const XrsProjSt
                                           const LaeaTmerc& k, double& x, double& y) {
   // laea_inv's first half, with its two constant divisions as products by
   // reciprocals set up once per thread and the radius from sqrt / rsqrt of
-  // one sum of squares (each an ulp from the two-step pipeline's xx, rho and
-  // a; its `small` / `bad` thresholds are not that close to any point: 3 % and
-  // 1-2 % of the fused 2u gather, profiles/r05_2u_int32_recip_ab.jsonl,
-  // r05_2u_rho_rsqrt_ab.jsonl)
+  // one sum of squares (3 % and 1-2 % of the fused 2u gather,
+  // profiles/r05_2u_int32_recip_ab.jsonl, r05_2u_rho_rsqrt_ab.jsonl).  Those
+  // values are within 8 ulps of the two-step pipeline's xx, rho and a; the
+  // `small` / `bad` DECISIONS are the two-step pipeline's own: wherever rho
+  // or a lies within 2^-46 (relative, > 60 ulps) of its threshold they are
+  // re-taken with laea_inv's operations (x / dd, hypot, 0.5 * rho / rq), so
+  // a point never flips between data and fill (ADVICE r05;
+  // tests/test_transform_gpu.py::test_fused_laea_tmerc_decisions_at_thresholds).
   double xx = (x - s0.x0) * s0.ra, yy = (y - s0.y0) * s0.ra;
+  const double xx_in = xx;
   xx = xx * k.inv_dd;
   yy = yy * s0.dd;
-  // |xx|, |yy| are a few earth radii at most: no scaling needed; rho and
-  // its reciprocal from one sum of squares (an ulp from hypot / a division)
+  // |xx|, |yy| are a few earth radii at most: no scaling needed
   const double r2s = xx * xx + yy * yy;
   const double rho = sqrt(r2s);
-  const bool small = rho < kEps10;
+  bool small = rho < kEps10;
+  bool bad = (small ? 1.0 : rho) * k.half_inv_rq > 1.0;
+  if (fabs(rho * k.half_inv_rq - 1.0) < 0x1p-46 || fabs(rho - kEps10) < 0x1p-46 * kEps10) {
+    const double rx = hypot(xx_in / s0.dd, yy);   // laea_inv's x / dd, y * dd, hypot
+    small = rx < kEps10;
+    bad = 0.5 * (small ? 1.0 : rx) / s0.rq > 1.0;
+  }
   const double rho_s = small ? 1.0 : rho;
   const double inv_rho_s = small ? 1.0 : rsqrt(r2s);
   const double a = rho_s * k.half_inv_rq;
-  const bool bad = a > 1.0;
-  const double ac = bad ? 1.0 : a;   // NaN stays NaN
+  const double ac = a > 1.0 ? 1.0 : a;   // NaN stays NaN; a bad point's value is replaced
   const double ca = sqrt((1.0 - ac) * (1.0 + ac));
   const double sCe = 2.0 * ac * ca;             // sin (2 asin ac)
   const double cCe = 1.0 - 2.0 * ac * ac;       // cos (2 asin ac)

@@ -367,16 +367,37 @@ ij_bboxes_kernel(BBoxArgs a, int64_t chunk) {
 // profiles/r04_rectify_k4_rows_ab.log).
 constexpr int kBoxBlockRows = 16;
 
-__device__ inline double wave_fmin_f64(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
-  return v;
+// Wave min / max of a double (NaN ignored unless every lane's is NaN, as
+// fmin / fmax), wave-uniform result.  DPP steps, no LDS round trip: each quad,
+// then each half-row and row of 16 lanes (quad_perm, row_half_mirror,
+// row_mirror), then rows 0+1 / 2+3 (row_bcast:15) and all four (row_bcast:31)
+// into lane 63.  Lanes a step does not write keep their value (min(v, v)).
+// (A butterfly of __shfl_xor — 12 dependent ds_bpermute round trips per
+// value — made the four block extremes the longest chain of K4's block.)
+template <int CTRL, int ROWS>
+__device__ inline double dpp_keep_f64(double v) {
+  const uint64_t b = __double_as_longlong(v);
+  const int lo = (int)(uint32_t)b, hi = (int)(uint32_t)(b >> 32);
+  const uint32_t l = (uint32_t)__builtin_amdgcn_update_dpp(lo, lo, CTRL, ROWS, 0xF, false);
+  const uint32_t h = (uint32_t)__builtin_amdgcn_update_dpp(hi, hi, CTRL, ROWS, 0xF, false);
+  return __longlong_as_double((int64_t)(((uint64_t)h << 32) | l));
 }
-__device__ inline double wave_fmax_f64(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
-  return v;
+template <bool MAX>
+__device__ inline double wave_ext_f64(double v) {
+  auto op = [](double x, double y) { return MAX ? fmax(x, y) : fmin(x, y); };
+  v = op(v, dpp_keep_f64<0xB1, 0xF>(v));    // quad_perm [1, 0, 3, 2]
+  v = op(v, dpp_keep_f64<0x4E, 0xF>(v));    // quad_perm [2, 3, 0, 1]
+  v = op(v, dpp_keep_f64<0x141, 0xF>(v));   // row_half_mirror
+  v = op(v, dpp_keep_f64<0x140, 0xF>(v));   // row_mirror
+  v = op(v, dpp_keep_f64<0x142, 0xA>(v));   // row_bcast:15 -> rows 1, 3
+  v = op(v, dpp_keep_f64<0x143, 0xC>(v));   // row_bcast:31 -> rows 2, 3
+  const uint64_t b = __double_as_longlong(v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, 63);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), 63);
+  return __longlong_as_double((int64_t)(((uint64_t)hi << 32) | lo));
 }
+__device__ inline double wave_fmin_f64(double v) { return wave_ext_f64<false>(v); }
+__device__ inline double wave_fmax_f64(double v) { return wave_ext_f64<true>(v); }
 
 template <bool SHARED>
 __global__ void __launch_bounds__(kThreads)

@@ -763,7 +763,8 @@ int launch_proj(const GatherArgs& a, const XrsProjStep& s0, const XrsProjStep& s
   // the same pipeline code as xrs_transform (proj::fast_kind picks it there too)
   int fast = proj::kFastNone;
   if constexpr (K0 == XRS_PROJ_LAEA_INV && K1 == XRS_PROJ_TMERC_FWD)
-    fast = proj::fast_kind(K0, K1, s0);
+    fast = xrs_testing_value(XRS_TESTING_PROJ_TWO_STEP) ? proj::kFastNone
+                                                        : proj::fast_kind(K0, K1, s0);
   if (fast == proj::kFastObliq)
     launch_proj_mode<K0, K1, proj::kFastObliq>(nb, a, s0, s1, mode, stream);
   else if (fast == proj::kFastEquit)

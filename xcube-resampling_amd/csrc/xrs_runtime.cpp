@@ -74,33 +74,26 @@ extern "C" int xrs_host_register(void* ptr, int64_t bytes) {
   return XRS_OK;
 }
 
-extern "C" int xrs_host_unregister(void* ptr) {
-  if (!ptr) {
-    xrs_set_error("xrs_host_unregister: invalid argument");
+// The caller names the streams that used the range (include/xrs.h): each is
+// synchronised before the pages are unpinned, so no copy queued on them
+// outlives the pinning, and nothing else waits — in a multi-device process
+// other threads' streams keep running (a device-wide drain stalled them).
+extern "C" int xrs_host_unregister(void* ptr, void* const* streams, int64_t nstreams) {
+  if (!ptr || nstreams < 1 || nstreams > 64 || !streams) {
+    xrs_set_error("xrs_host_unregister: invalid argument (ptr and 1..64 streams required, "
+                  "got %lld)", (long long)nstreams);
     return XRS_ERR_ARG;
   }
-  // A copy queued on any stream of any device (the band pipelines use three
-  // streams, a multi-GPU process one or more per device) may still read or
-  // write the range: drain every visible device before the pages are
-  // unpinned, so no DMA outlives the registration it was issued under.  (A
-  // binding that knows the streams should synchronise those and keep the
-  // registration out of graph-capture windows: a device drain stalls
-  // unrelated work, include/xrs.h.)
-  int ndev = 0, cur = 0;
-  hipError_t e = hipGetDeviceCount(&ndev);
-  if (e == hipSuccess) e = hipGetDevice(&cur);
-  for (int d = 0; e == hipSuccess && d < ndev; ++d) {
-    e = hipSetDevice(d);
-    if (e == hipSuccess) e = hipDeviceSynchronize();
+  for (int64_t k = 0; k < nstreams; ++k) {
+    const hipError_t e = hipStreamSynchronize(static_cast<hipStream_t>(streams[k]));
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      xrs_set_error("xrs_host_unregister: synchronising stream %lld: %s", (long long)k,
+                    hipGetErrorString(e));
+      return XRS_ERR_HIP;
+    }
   }
-  const hipError_t er = hipSetDevice(cur);
-  if (e == hipSuccess) e = er;
-  if (e != hipSuccess) {
-    (void)hipGetLastError();
-    xrs_set_error("xrs_host_unregister: draining the devices: %s", hipGetErrorString(e));
-    return XRS_ERR_HIP;
-  }
-  e = hipHostUnregister(ptr);
+  const hipError_t e = hipHostUnregister(ptr);
   if (e != hipSuccess) {
     (void)hipGetLastError();
     xrs_set_error("hipHostUnregister: %s", hipGetErrorString(e));

@@ -68,7 +68,8 @@ int launch_pipeline(bool grid, int nb, hipStream_t st, const double* x, const do
                     int64_t w, int64_t h, const XrsProjStep& s0, const XrsProjStep& s1,
                     double* ox, double* oy) {
   if constexpr (K0 == XRS_PROJ_LAEA_INV && K1 == XRS_PROJ_TMERC_FWD) {
-    const int fast = proj::fast_kind(K0, K1, s0);
+    const int fast = xrs_testing_value(XRS_TESTING_PROJ_TWO_STEP) ? proj::kFastNone
+                                                                  : proj::fast_kind(K0, K1, s0);
     if (fast == proj::kFastObliq) {
       launch_fast<K0, K1, proj::kFastObliq>(grid, nb, st, x, y, w, h, s0, s1, ox, oy);
       return XRS_OK;

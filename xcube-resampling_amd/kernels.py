@@ -10,7 +10,9 @@ rectify.py is built on them.
 
 from __future__ import annotations
 
+import collections
 import ctypes
+import threading
 
 import numpy as np
 
@@ -493,7 +495,9 @@ def rectify_var(ij, src, interp: str, fill, stream=None, rows=None, out=None,
     return out
 
 
-_WORKSPACES: dict = {}
+_WORKSPACES: "collections.OrderedDict" = collections.OrderedDict()
+_WORKSPACES_MAX = 8          # (device, stream) entries kept (least recently used dropped)
+_WORKSPACES_LOCK = threading.Lock()
 
 
 def _workspace(device, nbytes: int, stream=None):
@@ -501,15 +505,27 @@ def _workspace(device, nbytes: int, stream=None):
     reused across calls.  Keyed by (device, stream) and allocated on that
     stream: launches of one stream are ordered, so they may share it, while
     partitions running on other streams of the same device (multidevice,
-    a threaded chunk scheduler) each get their own."""
+    a threaded chunk scheduler) each get their own.  At most _WORKSPACES_MAX
+    entries are kept, least recently used dropped first (the band pipelines
+    and multi-device parts take a fresh pool stream per call): a
+    dropped workspace returns to torch's caching allocator in the pool of the
+    stream it was allocated on, so only later work on that same stream — ordered
+    after the launches that used it — can reuse its memory."""
     t = torch()
     s = stream if stream is not None else t.cuda.current_stream(device)
     key = (str(device), int(s.cuda_stream))
-    ws = _WORKSPACES.get(key)
+    with _WORKSPACES_LOCK:
+        ws = _WORKSPACES.get(key)
+        if ws is not None:
+            _WORKSPACES.move_to_end(key)
     if ws is None or ws.numel() < nbytes:
         with t.cuda.stream(s):
             ws = t.empty(max(nbytes, 1), dtype=t.uint8, device=device)
-        _WORKSPACES[key] = ws
+        with _WORKSPACES_LOCK:
+            _WORKSPACES[key] = ws
+            _WORKSPACES.move_to_end(key)
+            while len(_WORKSPACES) > _WORKSPACES_MAX:
+                _WORKSPACES.popitem(last=False)
     return ws
 
 

@@ -55,7 +55,9 @@ def normalize(devices):
             out.append(t.device("cuda", d))
         else:
             d = t.device(d)
-            out.append(d if d.index is not None else t.device("cuda", 0))
+            # an index-less "cuda" is torch's current device, resolved now (under
+            # torch.cuda.set_device(k) it is GPU k, not 0 — ADVICE r05)
+            out.append(d if d.index is not None else t.device("cuda", t.cuda.current_device()))
     return out
 
 
