@@ -184,6 +184,12 @@ int xrs_reproject(const void* src, int src_dtype, int64_t n, int64_t src_h,
  *   chunk's input slice; -1 = none.
  * recover_nan: affine.py:344-360 (NaN -> 0 image / (1 - mask) image ratio;
  *   the host decides it with xrs_any_nan as the reference does with da.any).
+ * run_weights: a speed hint for square 2/4/8 float coarsens of order 1 —
+ *   nonzero when the div-x grid has scale 1 but offsets off the integral
+ *   layout (a target grid not aligned to the source): the contiguous-run
+ *   kernel with fractional weights (K3w) instead of the integral-run one
+ *   (K3i).  Results are identical either way (each falls back to the exact
+ *   path wherever its runs break).
  * workspace: xrs_affine_workspace_size(out_h*div_y, out_w*div_x) bytes.
  * ------------------------------------------------------------------------- */
 int64_t xrs_affine_workspace_size(int64_t inter_h, int64_t inter_w);
@@ -195,7 +201,7 @@ int xrs_affine(const void* src, int src_dtype, int64_t nt, int64_t src_h, int64_
                const int64_t* rel_y, const int64_t* len_y, const double* off_y,
                int64_t chunk_x, const int64_t* rel_x, const int64_t* len_x,
                const double* off_x, const int64_t* t_next, double cval, int recover_nan,
-               void* workspace, int64_t workspace_bytes, void* stream);
+               int run_weights, void* workspace, int64_t workspace_bytes, void* stream);
 
 /* -------------------------------------------------------------------------
  * xrs_coarsen — replaces da.coarsen(agg, array, {ndim-2: div_y, ndim-1:

@@ -332,3 +332,50 @@ def test_k2_slice_groups_match_oracle(nt, interp, dtype):
         ref = affine_ref.resample_array(a[t:t + 1], m, (1, n, n), (1, 40, 48), interp, "first",
                                         False, fill)
         assert_bitwise_equal(got[t] if nt > 1 else got, np.asarray(ref)[0], f"slice {t}")
+
+
+@pytest.mark.parametrize("dtype,nd", [(np.float32, 2), (np.float64, 2), (np.float32, 3),
+                                      (np.float64, 3)])
+def test_fractional_coarsen_k3w_matches_oracle(dtype, nd):
+    """K3w (square 2/4/8 order-1 coarsens whose div-x grid has scale 1 but a
+    fractional offset: contiguous taps, fractional weights — a target grid not
+    aligned to the source, affine.py:277-313) is bit-exact with the oracle for
+    every fused reducer, NaN / +-inf / -0.0 taps, the zero-weight time
+    neighbour of 3-D inputs, targets reaching past the source (cval, mirrored
+    last row / column through the exact path) and chunk edges; the plan's
+    hint selects it (AffinePlan.run_weights) and the integral-run kernel gives
+    the same bits on the same grids."""
+    import xcube_resampling_amd.affine as A
+    from oracle import affine_ref
+
+    rng = np.random.default_rng(777)
+    lead = (2,) if nd == 3 else ()
+    cases = [(4, (0.5, 0.25), (40, 60), (20, 60), "mean"),
+             (4, (-1.3, 2.7), (33, 70), (33, 35), "sum"),
+             (2, (0.3, -0.6), (50, 130), (25, 64), "max"),
+             (2, (1.75, 0.5), (21, 90), (21, 90), "min"),
+             (8, (0.125, 3.5), (12, 40), (6, 40), "mean"),
+             (4, (2.5, 0.5), (30, 50), (30, 50), "prod"),
+             (4, (0.5, 1.5), (30, 50), (15, 50), "count")]
+    for d, (ox, oy), oshape, tile, agg in cases:
+        if d == 8 and dtype == np.float64:
+            continue   # (no K3i / K3w instance: 9 rows of 8 doubles)
+        shp = lead + (oshape[0] * d + 3, oshape[1] * d + 2)
+        a = (rng.random(shp) * 4 - 2).astype(dtype)
+        flat = a.reshape(-1)
+        idx = rng.choice(flat.size, max(4, flat.size // 300), replace=False)
+        q = idx.size // 4
+        flat[idx[:q]] = np.nan
+        flat[idx[q:2 * q]] = np.inf
+        flat[idx[2 * q:3 * q]] = -np.inf
+        flat[idx[3 * q:]] = -0.0
+        m = ((float(d), 0.0, ox), (0.0, float(d), oy))
+        ochunks = tuple(1 for _ in lead) + tile
+        plan = A.plan_affine((1,) * (3 - nd) + a.shape, np.dtype(dtype), m,
+                             (1,) * (3 - nd) + lead + oshape, (1,) * (3 - nd) + ochunks, 1, agg,
+                             False, np.nan)
+        assert plan.run_weights, (d, ox, oy)
+        ref = affine_ref.resample_array(a, m, lead + oshape, ochunks, 1, agg, False, np.nan)
+        got = A._resample_array(a, None, None, m, lead + oshape, ochunks, 1, agg, False, np.nan)
+        got = got if isinstance(got, np.ndarray) else got.cpu().numpy()
+        assert_bitwise_equal(got, np.asarray(ref), f"k3w {dtype} d={d} off={ox},{oy} {agg}")

@@ -107,7 +107,7 @@ _SIGNATURES = {
         _c_i64, _c_i64, _c_int, _c_int, _c_dbl, _c_dbl,                          # div, agg, order, scale
         _c_i64, _c_ptr, _c_ptr, _c_ptr,                                          # y chunks
         _c_i64, _c_ptr, _c_ptr, _c_ptr,                                          # x chunks
-        _c_ptr, _c_dbl, _c_int, _c_ptr, _c_i64, _c_ptr,                          # t_next .. stream
+        _c_ptr, _c_dbl, _c_int, _c_int, _c_ptr, _c_i64, _c_ptr,                  # t_next .. stream
     ]),
     "xrs_coarsen_workspace_size": (_c_i64, [_c_i64]),
     "xrs_coarsen": (_c_int, [

@@ -203,6 +203,20 @@ class AffinePlan:
     post_chunks: tuple | None = None   # dask chunk ids (t, y, x) for float mode
     _cache: dict = field(default_factory=dict, repr=False)
 
+    @property
+    def run_weights(self) -> bool:
+        """xrs_affine's K3w hint: an order-1 coarsen whose div-x grid has scale 1
+        on both axes with some chunk offset off the integral layout (a target
+        grid not aligned to the source: contiguous taps, fractional weights).
+        Only the kernel choice depends on it, never the result."""
+        if self.order != 1 or (self.div_y == 1 and self.div_x == 1):
+            return False
+        if self.scale_y != 1.0 or self.scale_x != 1.0:
+            return False
+        offs = np.concatenate([np.asarray(self.off_y, np.float64).ravel(),
+                               np.asarray(self.off_x, np.float64).ravel()])
+        return bool(np.any(offs != np.floor(offs)))
+
     def device_tables(self, device) -> dict:
         key = str(device)
         tabs = self._cache.get(key)

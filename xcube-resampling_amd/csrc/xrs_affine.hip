@@ -109,12 +109,21 @@ __device__ inline bool integral_entry(const AxisTab& e, int32_t g_first, int k) 
          (ORDER == 0 || (e.w1 == 0.0 && e.g1 == e.g0 + 1));
 }
 
+// K3w's run entries: contiguous source taps (g0 = first + k, order 1: the
+// second tap at g0 + 1, not mirrored) with any weights
+template <int ORDER>
+__device__ inline bool run_entry(const AxisTab& e, int32_t g_first, int k, bool weighted) {
+  if (!weighted) return integral_entry<ORDER>(e, g_first, k);
+  return e.g0 >= 0 && e.g0 == g_first + k && (ORDER == 0 || e.g1 == e.g0 + 1);
+}
+
 // With `runs` (K3i candidates, div dy x dx): also K3i's run records — per
 // output row / column the first source index of its integral-contiguous run
 // of entries (entry k of a pixel's run = first entry + k, order 1: weight 0
 // and the next tap at +1), -1 where the layout breaks (the image's last row /
 // column, where scipy mirrors the tap, always breaks it: K3i serves such
-// pixels through its exact path).  Block 0 also sets K3i's counters: the
+// pixels through its exact path).  `weighted` (K3w): the records of contiguous
+// runs with any weights (run_entry).  Block 0 also sets K3i's counters: the
 // slow-pixel count to 0 and — with time neighbours — whether any slice's
 // zero-weight neighbour is another slice (plain stores: no memset before
 // this launch; K3i and its finish run after it on the same stream).
@@ -124,7 +133,7 @@ affine_tables_kernel(AxisChunks ay, AxisChunks ax, AxisTab* __restrict__ ytab,
                      AxisTab* __restrict__ xtab, int64_t dy, int64_t dx,
                      int32_t* __restrict__ counters, const int64_t* __restrict__ t_next,
                      int64_t nt, bool check_self, int32_t* __restrict__ yrun,
-                     int32_t* __restrict__ xrun, bool wave_runs) {
+                     int32_t* __restrict__ xrun, bool wave_runs, bool weighted) {
   if (counters && blockIdx.x == 0) {
     bool other = false;   // K3i: a zero-weight time neighbour other than the slice?
     if (check_self)
@@ -151,13 +160,13 @@ affine_tables_kernel(AxisChunks ay, AxisChunks ax, AxisTab* __restrict__ ytab,
       const int lane = (int)(threadIdx.x & 63);
       const int k = (int)(o % d);
       const int32_t g_first = __shfl(e.g0, lane - k);
-      const uint64_t bad = __ballot(!integral_entry<ORDER>(e, g_first, k));
+      const uint64_t bad = __ballot(!run_entry<ORDER>(e, g_first, k, weighted));
       if (k == 0)
         (is_y ? yrun : xrun)[o / d] = ((bad >> lane) & ((1ull << d) - 1)) == 0 ? e.g0 : -1;
     } else if (counters && o % d == 0) {   // K3i's run record of row / column o / d
-      bool ok = e.g0 >= 0 && integral_entry<ORDER>(e, e.g0, 0);
+      bool ok = e.g0 >= 0 && run_entry<ORDER>(e, e.g0, 0, weighted);
       for (int64_t j = 1; j < d && ok; ++j)
-        ok = integral_entry<ORDER>(axis_entry<ORDER>(ac, o + j), e.g0, (int)j);
+        ok = run_entry<ORDER>(axis_entry<ORDER>(ac, o + j), e.g0, (int)j, weighted);
       (is_y ? yrun : xrun)[o / d] = ok ? e.g0 : -1;
     }
   }
@@ -693,7 +702,13 @@ __device__ inline void load_run(const T* p, T (&v)[DX]) {
   for (int c = 0; c < DX; ++c) v[c] = p[c];
 }
 
-template <typename T, int ORDER, int D, bool TWO>
+// W (K3w): the runs are contiguous but the weights fractional (scale 1 at the
+// div-x grid, order 1, offsets off the integral layout — a target grid not
+// aligned to the source).  The same loads; each sub-sample is scipy's sum of
+// its 2 x 2 taps with the row / column weights of the tables (f64, scipy's
+// corner order, cast to T), so a pixel's only exact-path case is a broken run
+// (an image edge): non-finite taps are part of the formula.
+template <typename T, int ORDER, int D, bool TWO, bool W = false>
 __global__ void __launch_bounds__(kThreads)
 affine_reduce_integral_kernel(AffineArgs a, const int32_t* __restrict__ yrun,
                               const int32_t* __restrict__ xrun,
@@ -793,6 +808,16 @@ affine_reduce_integral_kernel(AffineArgs a, const int32_t* __restrict__ yrun,
         }
       }
     }
+    // K3w: the lane's column weights (its D entries of the x table)
+    double wx0[W ? D : 1], wx1[W ? D : 1];
+    if constexpr (W) {
+#pragma unroll
+      for (int si = 0; si < D; ++si) {
+        const AxisTab& e = a.xtab[(fast ? oi : 0) * D + si];
+        wx0[si] = e.w0;
+        wx1[si] = e.w1;
+      }
+    }
     bool overflow = false;
 #pragma unroll
     for (int q = 0; q < R; ++q) {
@@ -803,7 +828,60 @@ affine_reduce_integral_kernel(AffineArgs a, const int32_t* __restrict__ yrun,
       const bool lean = a.agg == AGG_MEAN || a.agg == AGG_SUM;
       const bool fq = fast && q < nfast;
       bool slow = !fq;
-      if (fq && lean) {
+      if constexpr (W) {
+        if (fq) {
+          double wy0[D], wy1[D];   // the output row's D row entries (wave-uniform)
+#pragma unroll
+          for (int sj = 0; sj < D; ++sj) {
+            const AxisTab& e = a.ytab[oj * D + sj];
+            wy0[sj] = e.w0;
+            wy1[sj] = e.w1;
+          }
+          // sub-sample (sj, si): Taps::eval's sum (affine_tables_kernel's
+          // weights, corner order, the zero-weight time neighbour after)
+          auto sub = [&](int sj, int si) -> T {
+            const int r = q * D + sj;
+            const T a00 = v[r][si], a01 = si + 1 < D ? v[r][si + 1] : nbv[r];
+            const T a10 = v[r + 1][si], a11 = si + 1 < D ? v[r + 1][si + 1] : nbv[r + 1];
+            double tt = 0.0;
+            tt += ((double)a00 * wy0[sj]) * wx0[si];
+            tt += ((double)a01 * wy0[sj]) * wx1[si];
+            tt += ((double)a10 * wy1[sj]) * wx0[si];
+            tt += ((double)a11 * wy1[sj]) * wx1[si];
+            if constexpr (T1) {
+              const T b00 = v1[r][si], b01 = si + 1 < D ? v1[r][si + 1] : nbv1[r];
+              const T b10 = v1[r + 1][si], b11 = si + 1 < D ? v1[r + 1][si + 1] : nbv1[r + 1];
+              tt += (((double)b00 * 0.0) * wy0[sj]) * wx0[si];
+              tt += (((double)b01 * 0.0) * wy0[sj]) * wx1[si];
+              tt += (((double)b10 * 0.0) * wy1[sj]) * wx0[si];
+              tt += (((double)b11 * 0.0) * wy1[sj]) * wx1[si];
+            }
+            return ScipyOut<T>::cast(tt);
+          };
+          if (lean) {   // nanmean / nansum: NaN sub-samples skipped
+            T total = (T)0;
+            int cnt = 0;
+#pragma unroll
+            for (int sj = 0; sj < D; ++sj)
+              total = total + pairwise_row<T>(D, [&](int si) {
+                const T x = sub(sj, si);
+                const bool nan = x != x;
+                cnt += nan ? 0 : 1;
+                return nan ? (T)0 : x;
+              });
+            const double res = a.agg == AGG_MEAN ? (double)(T)((double)total / (double)cnt)
+                                                 : (double)total;
+            store_any(a.dst, didx, a.dst_dtype, res, 0, false);
+          } else {
+            Fold<T> fold;
+#pragma unroll
+            for (int sj = 0; sj < D; ++sj)
+              fold.add_row(a.agg, D, [&](int si) { return sub(sj, si); });
+            fold.store(a, didx);
+          }
+          continue;
+        }
+      } else if (fq && lean) {
         // The values' sum equals numpy's whatever their zero signs (a signed
         // zero only flips the sign of a zero partial, and the total starts at
         // +0), so the -0 -> +0 map is not needed here.  Order 1: every value
@@ -982,10 +1060,13 @@ inline int64_t slow_capacity(int64_t ih, int64_t iw) { return 4 * (ih + iw) + 10
 
 template <typename T, typename I, int ORDER, bool RECOVER>
 int launch(const AffineArgs& a, const AxisChunks& ay, const AxisChunks& ax, AxisTab* ytab,
-           AxisTab* xtab, int32_t* nonint, hipStream_t st) {
+           AxisTab* xtab, int32_t* nonint, bool run_weights, hipStream_t st) {
   const bool direct = a.agg == AGG_NONE || a.agg == AGG_FIRST || a.agg == AGG_LAST ||
                       a.agg == AGG_CENTER;
   const bool k3i = !direct && integral_candidate<T, I, RECOVER>(a);
+  // K3w: the caller's hint that the runs are contiguous but not integral
+  // (scale 1, offsets off the integral layout); only the speed depends on it
+  const bool k3w = k3i && ORDER == 1 && run_weights;
   // counters (set by the tables kernel, no memset): nonint[1] a time neighbour
   // other than the slice, nonint[2] K3i's slow-pixel count (list of slow_cap
   // entries after them); one slice: its only possible neighbour is itself ->
@@ -1024,7 +1105,7 @@ int launch(const AffineArgs& a, const AxisChunks& ay, const AxisChunks& ax, Axis
                          ay.n % a.dy == 0 && ay.n % a.dx == 0 && ax.n % a.dx == 0;
   hipLaunchKernelGGL((affine_tables_kernel<ORDER>), dim3(nbt), dim3(kThreads), 0, st, ay, ax,
                      ytab, xtab, a.dy, a.dx, k3i ? nonint : nullptr, a.t_next, a.nt,
-                     t1_flag, yrun, xrun, wave_runs);
+                     t1_flag, yrun, xrun, wave_runs, k3w);
   XRS_HIP_CHECK(hipGetLastError());
   if (k3i) {
     const int64_t ntiles = ((a.out_w + kThreads - 1) / kThreads) *
@@ -1035,9 +1116,16 @@ int launch(const AffineArgs& a, const AxisChunks& ay, const AxisChunks& ax, Axis
     const int nb = grid_blocks(ntiles, 1, 1 << 24);
     if constexpr (std::is_floating_point<T>::value && std::is_same<T, I>::value && !RECOVER) {
 #define XRS_K3I(D, TWO, SELF)                                                             \
-  hipLaunchKernelGGL((affine_reduce_integral_kernel<T, ORDER, D, TWO>), dim3(nb),         \
-                     dim3(kThreads), 0, st, args, yrun, xrun, SELF, nonint + 2,          \
-                     slow_list, slow_cap)
+  do {                                                                                    \
+    if (k3w)                                                                              \
+      hipLaunchKernelGGL((affine_reduce_integral_kernel<T, ORDER, D, TWO, true>), dim3(nb), \
+                         dim3(kThreads), 0, st, args, yrun, xrun, SELF, nonint + 2,      \
+                         slow_list, slow_cap);                                           \
+    else                                                                                  \
+      hipLaunchKernelGGL((affine_reduce_integral_kernel<T, ORDER, D, TWO>), dim3(nb),     \
+                         dim3(kThreads), 0, st, args, yrun, xrun, SELF, nonint + 2,      \
+                         slow_list, slow_cap);                                           \
+  } while (0)
       // with time neighbours both instances launch; nonint[1] picks one
       constexpr bool O1 = ORDER == 1;
       int32_t* self = t1_flag ? nonint + 1 : nullptr;
@@ -1139,8 +1227,8 @@ extern "C" int xrs_affine(const void* src, int src_dtype, int64_t nt, int64_t sr
                           const int64_t* rel_y, const int64_t* len_y, const double* off_y,
                           int64_t chunk_x, const int64_t* rel_x, const int64_t* len_x,
                           const double* off_x, const int64_t* t_next, double cval,
-                          int recover_nan, void* workspace, int64_t workspace_bytes,
-                          void* stream) {
+                          int recover_nan, int run_weights, void* workspace,
+                          int64_t workspace_bytes, void* stream) {
   using namespace xrs;
   if (order != 0 && order != 1) {
     xrs_set_error("interp_methods must be one of 0, 1, 'nearest', 'bilinear'. Higher order is "
@@ -1177,14 +1265,15 @@ extern "C" int xrs_affine(const void* src, int src_dtype, int64_t nt, int64_t sr
   AxisTab* xtab = ytab + ih;
   int32_t* nonint = reinterpret_cast<int32_t*>(xtab + iw);
   hipStream_t st = static_cast<hipStream_t>(stream);
+  const bool rw = run_weights != 0;
   return dispatch_dtype(src_dtype, [&](auto tag) -> int {
     using T = decltype(tag);
     if constexpr (std::is_floating_point<T>::value) {
       if (recover_nan)
-        return order ? launch<T, double, 1, true>(a, ay, ax, ytab, xtab, nonint, st)
-                     : launch<T, double, 0, true>(a, ay, ax, ytab, xtab, nonint, st);
+        return order ? launch<T, double, 1, true>(a, ay, ax, ytab, xtab, nonint, rw, st)
+                     : launch<T, double, 0, true>(a, ay, ax, ytab, xtab, nonint, rw, st);
     }
-    return order ? launch<T, T, 1, false>(a, ay, ax, ytab, xtab, nonint, st)
-                 : launch<T, T, 0, false>(a, ay, ax, ytab, xtab, nonint, st);
+    return order ? launch<T, T, 1, false>(a, ay, ax, ytab, xtab, nonint, rw, st)
+                 : launch<T, T, 0, false>(a, ay, ax, ytab, xtab, nonint, rw, st);
   });
 }

@@ -575,7 +575,8 @@ def affine(src, plan, out=None, stream=None):
         plan.chunk_y, ptr(tabs["rel_y"]), ptr(tabs["len_y"]), ptr(tabs["off_y"]),
         plan.chunk_x, ptr(tabs["rel_x"]), ptr(tabs["len_x"]), ptr(tabs["off_x"]),
         ptr(tabs["t_next"]) if tabs["t_next"] is not None else None,
-        float(plan.cval), int(plan.recover_nan), ptr(ws), nbytes, stream_handle(device, stream))
+        float(plan.cval), int(plan.recover_nan), 1 if plan.run_weights else 0, ptr(ws), nbytes,
+        stream_handle(device, stream))
     _native.check(rc, "xrs_affine")
     return out
 
