@@ -387,7 +387,14 @@ def config2u(args):
 
 
 # ------------------------------------------------------------------ config 3
-def config3(args):
+def config3f(args):
+    """Config 3 with the target grid shifted by 0.3 / 0.6 source pixels (a
+    target not aligned to the source: the div-x grid has scale 1 and
+    fractional offsets, K3w)."""
+    config3(args, frac=True)
+
+
+def config3(args, frac=False):
     """Coarsen mean 4x4: 16384^2 f32 -> 4096^2 (bilinear upscale at scale 1 + nanmean)."""
     import torch
 
@@ -402,15 +409,22 @@ def config3(args):
     lat = n * res - (np.arange(n) + 0.5) * res
     sgm = xrs.GridMapping.from_coords(xrs.DataArray(lon, "lon", name="lon"),
                                       xrs.DataArray(lat, "lat", name="lat"), "EPSG:4326")
-    tgm = xrs.GridMapping.regular((n // k, n // k), (0, 0), res * k, "EPSG:4326")
+    if frac:   # shifted by (0.3, 0.6) source pixels, one output pixel short of the edge
+        tgm = xrs.GridMapping.regular((n // k - 1, n // k - 1), (0.3 * res, 0.6 * res), res * k,
+                                      "EPSG:4326")
+    else:
+        tgm = xrs.GridMapping.regular((n // k, n // k), (0, 0), res * k, "EPSG:4326")
     m = tgm.ij_transform_to(sgm)
-    assert m == ((4.0, 0.0, 0.0), (0.0, 4.0, 0.0)), m
+    if not frac:
+        assert m == ((4.0, 0.0, 0.0), (0.0, 4.0, 0.0)), m
+    no = tgm.width
     g = torch.Generator(device="cuda")
     g.manual_seed(20250905)
     src = torch.rand((1, n, n), generator=g, device="cuda", dtype=torch.float32)
     oc = (1, tgm.tile_height, tgm.tile_width)
-    plan = A.plan_affine(tuple(src.shape), np.dtype(np.float32), m, (1, n // k, n // k), oc, 1,
+    plan = A.plan_affine(tuple(src.shape), np.dtype(np.float32), m, (1, no, no), oc, 1,
                          "mean", False, np.nan)
+    assert plan.run_weights == frac
     out = kernels.affine(src, plan)
     # parity on a corner (the oracle on the full 1 GiB raster takes minutes)
     c = 1024
@@ -431,14 +445,19 @@ def config3(args):
         cj, ci = c
         blk = host[:, cj * cs:(cj + 1) * cs, ci * cs:(ci + 1) * cs]
         return affine_ref.resample_array(blk, m, (1, cs // k, cs // k), (1, cs // k, cs // k), 1,
-                                         "mean", False, np.nan).size
+                                         "mean", False, np.nan).size   # (frac: same work)
 
     cpu_v, dt, cores = _cpu_whole(lambda ex: sum(ex.map(task, chunks)), (n // k) ** 2)
     del host
-    _line(3, "coarsen mean 4x4: 16384x16384 f32 -> 4096x4096 (affine bilinear at the 4x grid "
-             "+ nanmean)", (n // k) ** 2, ms, wall, 4 * n * n + 4 * (n // k) ** 2,
-          "K3i affine_reduce_integral_kernel<float,1,4> (fused upscale+coarsen; edge pixels "
-          "via integral_slow_kernel)",
+    _line("3f" if frac else 3,
+          ("coarsen mean 4x4, target shifted by (0.3, 0.6) source px: 16384x16384 f32 -> "
+           "4095x4095 (affine bilinear at the 4x grid with fractional weights + nanmean)")
+          if frac else ("coarsen mean 4x4: 16384x16384 f32 -> 4096x4096 (affine bilinear at the "
+                        "4x grid + nanmean)"), no * no, ms, wall, 4 * n * n + 4 * no * no,
+          ("K3w affine_reduce_integral_kernel<float,1,4,false,true> (contiguous runs, fractional "
+           "weights; edge pixels via integral_slow_kernel)") if frac else
+          ("K3i affine_reduce_integral_kernel<float,1,4> (fused upscale+coarsen; edge pixels "
+           "via integral_slow_kernel)"),
           dict(value=round(cpu_v, 3), unit="Mpixels/s", cores=cores, kind="port",
                sample=f"the whole 16384^2 raster: its {len(chunks)} per-chunk tasks (a 2048^2 "
                       f"source chunk -> 512^2 each; scipy affine_transform + numpy nanmean in "
@@ -568,7 +587,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     args = ap.parse_args()
     for c in args.configs.split(","):
-        {"1": config1, "2": config2, "2u": config2u, "3": config3,
+        {"1": config1, "2": config2, "2u": config2u, "3": config3, "3f": config3f,
          "4": config4}[c.strip()](args)
 
 
