@@ -40,5 +40,13 @@ for arm in product $ARMS; do
   XRS_LIBRARY=$L timeout -k 10 200 python -u scripts/pmc_kernels.py --counters TCC_EA0_RDREQ_sum,TCC_EA0_RDREQ_32B_sum,TCC_EA0_RDREQ_64B_sum,TCC_EA0_RDREQ_128B_sum --kernels resolve -- scripts/time_rectify.py --fused --reps 3 > $O/pmc_rd_$arm.json 2> $O/pmc_rd_$arm.err || exit $?
   cut -c1-200 $O/pmc_rd_$arm.json
 done
+# the generic K3 (forced on the aligned grid; and a 3.5x downscale, div-x
+# grid at scale 0.875): time and one PMC pass each
+for mode in --generic --s35; do
+  timeout -k 10 120 python -u scripts/time_coarsen.py $mode 2>&1 | grep -v amdgpu.ids >> $O/coarsen.log || exit 1
+  tail -1 $O/coarsen.log
+  timeout -k 10 200 python -u scripts/pmc_kernels.py --counters SQ_WAVES,SQ_INSTS_VALU,SQ_INSTS_LDS,SQ_INSTS_VMEM_RD,SQ_WAIT_INST_LDS,SQ_LDS_BANK_CONFLICT,SQ_WAVE_CYCLES,SQ_BUSY_CYCLES --kernels affine_reduce_kernel,integral_finish,affine_reduce_integral -- scripts/time_coarsen.py $mode > $O/pmc_k3$mode.json 2> $O/pmc_k3$mode.err || exit $?
+  cut -c1-600 $O/pmc_k3$mode.json
+done
 timeout -k 10 1000 python -u scripts/bench_configs.py --configs 1,2,2u,3,3f,4 --cpu-seconds 6 > $O/configs.jsonl 2> $O/configs.err || { tail -20 $O/configs.err; exit 1; }
 cut -c1-200 $O/configs.jsonl

@@ -379,3 +379,44 @@ def test_fractional_coarsen_k3w_matches_oracle(dtype, nd):
         got = A._resample_array(a, None, None, m, lead + oshape, ochunks, 1, agg, False, np.nan)
         got = got if isinstance(got, np.ndarray) else got.cpu().numpy()
         assert_bitwise_equal(got, np.asarray(ref), f"k3w {dtype} d={d} off={ox},{oy} {agg}")
+
+
+@pytest.mark.parametrize("dtype,nd", [(np.float32, 2), (np.float64, 2), (np.float32, 3)])
+def test_generic_coarsen_k3d_matches_oracle(dtype, nd):
+    """K3d (the generic coarsen, one output pixel per lane: any div-x grid —
+    scales 1.7 ... 5.5 give divisors 2 ... 6 with the div-x grid off scale 1)
+    is bit-exact with the oracle (order 1: order 0 never coarsens,
+    affine.py:253-263) for several reducers, NaN /
+    +-inf / -0.0 taps, the zero-weight time neighbour of 3-D inputs and
+    targets reaching past the source; a divisor of 8 (float64: 5 and 6 too)
+    takes the LDS-band kernel, checked the same way."""
+    import xcube_resampling_amd.affine as A
+    from oracle import affine_ref
+
+    rng = np.random.default_rng(2468)
+    lead = (2,) if nd == 3 else ()
+    cases = [(1.7, (0.3, 0.2), (40, 70), (20, 70), 1, "mean"),
+             (2.5, (1.1, -0.4), (30, 50), (30, 25), 1, "max"),
+             (3.5, (0.0, 0.5), (24, 40), (12, 40), 1, "sum"),
+             (4.6, (2.2, 0.7), (16, 30), (16, 30), 1, "mean"),
+             (5.5, (0.5, 1.5), (14, 25), (7, 25), 1, "min"),
+             (3.25, (0.75, 0.25), (20, 33), (20, 33), 1, "count"),
+             (7.3, (0.4, 0.6), (10, 18), (10, 18), 1, "mean")]
+    for sc, (ox, oy), oshape, tile, order, agg in cases:
+        shp = lead + (int(oshape[0] * sc) + 4, int(oshape[1] * sc) + 3)
+        a = (rng.random(shp) * 4 - 2).astype(dtype)
+        flat = a.reshape(-1)
+        idx = rng.choice(flat.size, max(4, flat.size // 250), replace=False)
+        q = idx.size // 4
+        flat[idx[:q]] = np.nan
+        flat[idx[q:2 * q]] = np.inf
+        flat[idx[2 * q:3 * q]] = -np.inf
+        flat[idx[3 * q:]] = -0.0
+        m = ((sc, 0.0, ox), (0.0, sc, oy))
+        ochunks = tuple(1 for _ in lead) + tile
+        ref = affine_ref.resample_array(a, m, lead + oshape, ochunks, order, agg, False, np.nan)
+        got = A._resample_array(a, None, None, m, lead + oshape, ochunks, order, agg, False,
+                                np.nan)
+        got = got if isinstance(got, np.ndarray) else got.cpu().numpy()
+        assert_bitwise_equal(got, np.asarray(ref), f"k3d {dtype} scale={sc} off={ox},{oy} "
+                                                   f"order={order} {agg}")

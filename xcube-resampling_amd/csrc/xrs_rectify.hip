@@ -1425,19 +1425,26 @@ rectify_resolve_kernel(RectArgs a, FusedVar fv) {
   const int64_t n = a.dst_h * a.dst_w;
   const T tfill = FUSE ? Conv<T>::from_f64(fv.fill) : T{};
   // tile 0 has the full tile height (edge tiles are shorter)
-  const int64_t bands = (a.tiles[0].th + kResolveRows - 1) / kResolveRows;
-  const int64_t nitems = a.ntiles * bands;
+  // 2-D items: 128 columns x 4 waves x kResolveRows rows (a compact target
+  // patch, whose quads lie in a compact source patch: its corner rows are
+  // shared by the block's own waves instead of by bands on other XCDs)
+  constexpr int kSegW = 128, kBandH = 4 * kResolveRows;
+  const int64_t segs = (a.tiles[0].tw + kSegW - 1) / kSegW;
+  const int64_t bands = (a.tiles[0].th + kBandH - 1) / kBandH;
+  const int64_t nitems = a.ntiles * bands * segs;
   const double inv_w = 1.0 / (double)a.w;
   bool bad = false;
   for (int64_t it = blockIdx.x; it < nitems; it += gridDim.x) {
-    const int64_t t = it / bands;
-    const int32_t rb = (int32_t)(it - t * bands) * kResolveRows;
+    const int64_t t = it / (bands * segs);
+    const int64_t rem = it - t * bands * segs;
+    const int64_t band = rem / segs, seg = rem - band * segs;
+    const int32_t rb = (int32_t)band * kBandH + (int32_t)(threadIdx.x >> 6) * kResolveRows;
     const TileInfo ti = a.tiles[t];
     if (!tile_ok(a, ti)) {   // block-uniform
       bad = true;
       continue;
     }
-    if (rb >= ti.th) continue;
+    if (rb >= ti.th || seg * kSegW >= ti.tw) continue;   // wave-uniform
     const int32_t nr = min(kResolveRows, ti.th - rb);
     // a thread's columns di, di + kThreads of the item in pairs: the second
     // column's keys are requested with the first's, so their round trip is
@@ -1532,17 +1539,18 @@ rectify_resolve_kernel(RectArgs a, FusedVar fv) {
                                              bad);
       }
     };
-    for (int32_t d0 = threadIdx.x; d0 < ti.tw; d0 += 2 * kThreads) {
-      const int32_t d1 = d0 + kThreads;
-      const bool has1 = d1 < ti.tw;
+    {
+      const int32_t d0 = (int32_t)seg * kSegW + (int32_t)(threadIdx.x & 63);
+      const int32_t d1 = d0 + 64;
+      const bool has0 = d0 < ti.tw, has1 = d1 < ti.tw;
       const int64_t q0 = (int64_t)(ti.r0 + rb) * a.dst_w + ti.c0 + d0;
       uint32_t key0[kResolveRows], key1[kResolveRows];
 #pragma unroll
       for (int r = 0; r < kResolveRows; ++r) {
-        key0[r] = r < nr ? a.keys[q0 + r * a.dst_w] : 0xFFFFFFFFu;
-        key1[r] = r < nr && has1 ? a.keys[q0 + kThreads + r * a.dst_w] : 0xFFFFFFFFu;
+        key0[r] = r < nr && has0 ? a.keys[q0 + r * a.dst_w] : 0xFFFFFFFFu;
+        key1[r] = r < nr && has1 ? a.keys[q0 + 64 + r * a.dst_w] : 0xFFFFFFFFu;
       }
-      column(d0, key0);
+      if (has0) column(d0, key0);
       if (has1) column(d1, key1);
     }
   }
