@@ -663,91 +663,6 @@ affine_reduce_kernel(AffineArgs a, const AxisTab* __restrict__ ytab,
   reduce_body<T, I, ORDER, RECOVER>(a, ytab, xtab, group);
 }
 
-// ---- K3d: the generic coarsen, one output pixel per lane (round 6) -------------
-// affine.py:277-313 for any div-x grid (a 3.5x downscale: div 4, the div-x grid
-// at scale 0.875), float data: a lane evaluates its pixel's DX x dy
-// sub-samples itself — its DX column entries loaded once per item, each
-// sub-row's entry wave-uniform, the DX sub-samples of kK3dRows sub-rows in
-// flight together (Taps: scipy's sum, exactly as K3) — and folds them in
-// numpy's order (Fold).  No LDS band, no barrier: reduce_body's two phases
-// per 64 x 4 tile ran at 1320 VALU per output pixel and 16 K waves in all
-// (profiles/r06d_pmc_generic_k3_*).  Lanes on consecutive output columns read
-// sub-samples DX columns apart; the other sub-columns' loads hit the same
-// lines in L1.
-constexpr int kK3dItemRows = 2;   // output rows per item (the column entries reused)
-constexpr int kK3dRows = 1;       // sub-rows whose taps are in flight together
-
-template <typename T, typename I, int ORDER, bool RECOVER, bool HAS_T1, int DX>
-__device__ inline void k3d_pixel(const AffineArgs& a, const Src<T>& p, const AxisTab (&ex)[DX],
-                                 int64_t t, int64_t oj, int64_t oi) {
-  const int ny = (int)a.dy;
-  Fold<I> fold;
-  for (int s0 = 0; s0 < ny; s0 += kK3dRows) {   // wave-uniform
-    AxisTab ey[kK3dRows];
-    Taps<T> tp[kK3dRows][DX];
-#pragma unroll
-    for (int q = 0; q < kK3dRows; ++q) {
-      ey[q] = a.ytab[oj * ny + min(s0 + q, ny - 1)];
-#pragma unroll
-      for (int si = 0; si < DX; ++si) tp[q][si].template load<ORDER, HAS_T1>(p, ey[q], ex[si]);
-    }
-#pragma unroll
-    for (int q = 0; q < kK3dRows; ++q) {
-      if (s0 + q >= ny) break;
-      I v[DX];
-#pragma unroll
-      for (int si = 0; si < DX; ++si)
-        v[si] = tp[q][si].template eval<I, ORDER, RECOVER, HAS_T1>(ey[q], ex[si], a.cval);
-      fold.add_row(a.agg, DX, [&](int si) { return v[si]; });
-    }
-  }
-  fold.store(a, t * a.dst_st + oj * a.dst_sy + oi);
-}
-
-template <typename T, typename I, int ORDER, bool RECOVER, int DX>
-__device__ inline void k3d_body(const AffineArgs& a) {
-  const int64_t ntx = (a.out_w + kThreads - 1) / kThreads;
-  const int64_t nty = (a.out_h + kK3dItemRows - 1) / kK3dItemRows;
-  const int64_t nwork = ntx * nty * a.nt;
-  // whole bands of items to the XCDs in turn (K3i's deal)
-  for (XcdGroups sg = xcd_groups(nwork, ntx);; sg.i += sg.step) {
-    const int64_t w = sg.item();
-    if (w >= nwork) break;
-    const int64_t t = w / (ntx * nty);
-    const int64_t rem = w - t * ntx * nty;
-    const int64_t tj = rem / ntx, ti = rem - tj * ntx;
-    const int64_t oi = ti * kThreads + threadIdx.x;
-    if (oi >= a.out_w) continue;   // (no cross-lane operation below)
-    const int64_t t1 = a.t_next ? a.t_next[t] : -1;
-    Src<T> p;
-    p.g0 = static_cast<const T*>(a.src) + t * a.src_st;
-    p.g1 = t1 >= 0 ? static_cast<const T*>(a.src) + t1 * a.src_st : p.g0;
-    p.sy = a.src_sy;
-    AxisTab ex[DX];
-#pragma unroll
-    for (int si = 0; si < DX; ++si) ex[si] = a.xtab[oi * DX + si];
-    for (int q = 0; q < kK3dItemRows; ++q) {
-      const int64_t oj = tj * kK3dItemRows + q;
-      if (oj >= a.out_h) break;
-      if (ORDER == 1 && t1 >= 0) k3d_pixel<T, I, ORDER, RECOVER, true, DX>(a, p, ex, t, oj, oi);
-      else k3d_pixel<T, I, ORDER, RECOVER, false, DX>(a, p, ex, t, oj, oi);
-    }
-  }
-}
-
-template <typename T, typename I, int ORDER, bool RECOVER, int DX>
-__global__ void __launch_bounds__(kThreads, 4)   // <= 128 VGPRs
-affine_k3d_kernel(AffineArgs a) {
-  k3d_body<T, I, ORDER, RECOVER, DX>(a);
-}
-
-// K3d serves float data without recover_nans for div_x 2..6 (float64: 2..4;
-// wider pixels spill under the 128-VGPR bound: DX = 8 spills 44 / 112 VGPRs)
-template <typename T, typename I, bool RECOVER>
-inline bool k3d_ok(int64_t dx) {
-  return std::is_floating_point<T>::value && std::is_same<T, I>::value && !RECOVER && dx >= 2 &&
-         dx <= (sizeof(T) == 4 ? 6 : 4);
-}
 
 // K3i: coarsen reducers when every sub-sample of a pixel sits on a source
 // pixel (scale 1 at the div-x grid with integral offsets — every aligned
@@ -1162,7 +1077,10 @@ int launch(const AffineArgs& a, const AxisChunks& ay, const AxisChunks& ax, Axis
   const bool direct = a.agg == AGG_NONE || a.agg == AGG_FIRST || a.agg == AGG_LAST ||
                       a.agg == AGG_CENTER;
   // K3i / K3w need scale 1 at the div-x grid (div = ceil(scale) >= scale, so
-  // it is an integer only at 1); any other grid goes straight to K3d
+  // it is an integer only at 1); any other grid goes straight to the generic
+  // K3 — K3i would only overflow its slow list, and its appends to the one
+  // counter serialised: 3.93 of 5.04 ms for a 3.5x downscale of 16384^2
+  // (profiles/r06e_*, r06f_*)
   const bool k3i = !direct && integral_candidate<T, I, RECOVER>(a) && ay.scale == 1.0 &&
                    ax.scale == 1.0;
   // K3w: the caller's hint that the runs are contiguous but not integral
@@ -1267,30 +1185,6 @@ int launch(const AffineArgs& a, const AxisChunks& ay, const AxisChunks& ax, Axis
       else if (a.dx == 4) XRS_K3F(4);
       else if constexpr (sizeof(T) == 4) { if (a.dx == 8) XRS_K3F(8); }
 #undef XRS_K3F
-    }
-  }
-  if constexpr (std::is_floating_point<T>::value && std::is_same<T, I>::value && !RECOVER) {
-    if (!launched && k3d_ok<T, I, RECOVER>(a.dx)) {
-      const int64_t nwork = ((a.out_w + kThreads - 1) / kThreads) *
-                            ((a.out_h + kK3dItemRows - 1) / kK3dItemRows) * a.nt;
-      const int nbd = grid_blocks(nwork, 1, 1 << 24);
-      switch (a.dx) {
-#define XRS_K3D(DX)                                                                            \
-  case DX:                                                                                     \
-    hipLaunchKernelGGL((affine_k3d_kernel<T, I, ORDER, RECOVER, DX>), dim3(nbd), dim3(kThreads), \
-                       0, st, args);                                                           \
-    break;
-        XRS_K3D(2) XRS_K3D(3) XRS_K3D(4)
-        default:
-          if constexpr (sizeof(T) == 4) {
-            if (a.dx == 5) hipLaunchKernelGGL((affine_k3d_kernel<T, I, ORDER, RECOVER, 5>),
-                                              dim3(nbd), dim3(kThreads), 0, st, args);
-            else hipLaunchKernelGGL((affine_k3d_kernel<T, I, ORDER, RECOVER, 6>), dim3(nbd),
-                                    dim3(kThreads), 0, st, args);
-          }
-#undef XRS_K3D
-      }
-      launched = true;
     }
   }
   if (!launched)
