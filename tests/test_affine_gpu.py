@@ -382,14 +382,14 @@ def test_fractional_coarsen_k3w_matches_oracle(dtype, nd):
 
 
 @pytest.mark.parametrize("dtype,nd", [(np.float32, 2), (np.float64, 2), (np.float32, 3)])
-def test_generic_coarsen_k3d_matches_oracle(dtype, nd):
-    """K3d (the generic coarsen, one output pixel per lane: any div-x grid —
-    scales 1.7 ... 5.5 give divisors 2 ... 6 with the div-x grid off scale 1)
-    is bit-exact with the oracle (order 1: order 0 never coarsens,
-    affine.py:253-263) for several reducers, NaN /
-    +-inf / -0.0 taps, the zero-weight time neighbour of 3-D inputs and
-    targets reaching past the source; a divisor of 8 (float64: 5 and 6 too)
-    takes the LDS-band kernel, checked the same way."""
+def test_generic_coarsen_non_integer_factors_matches_oracle(dtype, nd):
+    """The generic coarsen (affine.py:277-313 for non-integer factors: scales
+    1.7 ... 7.3 give divisors 2 ... 8 with the div-x grid off scale 1, which
+    since round 6 skip K3i / K3w and go straight to the LDS-band K3) is
+    bit-exact with the oracle (order 1: order 0 never coarsens,
+    affine.py:253-263) for several reducers, NaN / +-inf / -0.0 taps, the
+    zero-weight time neighbour of 3-D inputs and targets reaching past the
+    source."""
     import xcube_resampling_amd.affine as A
     from oracle import affine_ref
 
@@ -418,5 +418,5 @@ def test_generic_coarsen_k3d_matches_oracle(dtype, nd):
         got = A._resample_array(a, None, None, m, lead + oshape, ochunks, order, agg, False,
                                 np.nan)
         got = got if isinstance(got, np.ndarray) else got.cpu().numpy()
-        assert_bitwise_equal(got, np.asarray(ref), f"k3d {dtype} scale={sc} off={ox},{oy} "
+        assert_bitwise_equal(got, np.asarray(ref), f"generic {dtype} scale={sc} off={ox},{oy} "
                                                    f"order={order} {agg}")
