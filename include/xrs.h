@@ -369,6 +369,9 @@ int xrs_rectify_var(const double* ij, int64_t ij_sn, int64_t dst_h, int64_t dst_
  *   XRS_TESTING_PROJ_TWO_STEP             1: LAEA inverse -> tmerc forward runs as
  *                                         two library-transcendental steps instead
  *                                         of the fused sine / cosine pipeline
+ *   XRS_TESTING_RECTIFY_COMPACT           1 / 2: K5's claim walks every tile's
+ *                                         windows compacted across the wave / per
+ *                                         lane (0: chosen per tile)
  * Returns the previous value (or XRS_ERR_ARG for an unknown knob).
  * ------------------------------------------------------------------------- */
 #define XRS_TESTING_REPROJECT_BAND 1
@@ -378,7 +381,8 @@ int xrs_rectify_var(const double* ij, int64_t ij_sn, int64_t dst_h, int64_t dst_
 #define XRS_TESTING_RECTIFY_MARGIN 5
 #define XRS_TESTING_RECTIFY_PLAIN_KEYS 7
 #define XRS_TESTING_PROJ_TWO_STEP 8
-#define XRS_TESTING_NUM_KNOBS 9
+#define XRS_TESTING_RECTIFY_COMPACT 9
+#define XRS_TESTING_NUM_KNOBS 10
 int64_t xrs_testing_set(int knob, int64_t value);
 
 /* ---- coordinate transformation (reproject.py:472-496, rectify.py:182-231) --

@@ -2,7 +2,10 @@
 resolve, K6 nearest): the workload of scripts/bench_configs.py config4, for
 rocprofv3 --kernel-trace --stats runs of kernel variants.  --fused samples the
 variable inside K5's resolve pass (xrs_rectify_ij_var, no ij image written).
-    python scripts/time_rectify.py [--reps N] [--fused] [--interp nearest|bilinear|triangular]"""
+--res-div F divides the target resolution by F (F^2 more target pixels per
+source quad: larger claim windows).
+    python scripts/time_rectify.py [--reps N] [--fused] [--interp nearest|bilinear|triangular]
+                                   [--res-div F] [--compact 0|1|2]"""
 
 from __future__ import annotations
 
@@ -22,11 +25,14 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--fused", action="store_true")
     ap.add_argument("--interp", default="nearest", choices=["nearest", "bilinear", "triangular"])
+    ap.add_argument("--res-div", type=float, default=1.0)
+    ap.add_argument("--compact", type=int, default=0,
+                    help="claim walk: 0 per tile (product), 1 compacted, 2 per lane")
     args = ap.parse_args()
     import torch
 
     import xcube_resampling_amd as xrs
-    from xcube_resampling_amd import kernels
+    from xcube_resampling_amd import _native, kernels
     from xcube_resampling_amd import rectify as R
 
     w, h = 4000, 4800
@@ -37,7 +43,7 @@ def main():
         + rng.normal(0, 0.05 * 0.0027, (h, w))
     lon = 5 + 0.0045 * i + 0.0009 * j + rng.normal(0, 0.05 * 0.0045, (h, w))
     var = rng.random((1, h, w), dtype=np.float32)
-    res = 0.0027
+    res = 0.0027 / args.res_div
     x0, y0 = float(np.floor(lon.min() / res) * res), float(np.floor(lat.min() / res) * res)
     tw, th = int(np.ceil((lon.max() - x0) / res)), int(np.ceil((lat.max() - y0) / res))
     tgm = xrs.GridMapping.regular((tw, th), (x0, y0), res, "EPSG:4326", tile_size=512)
@@ -48,6 +54,8 @@ def main():
     ntx = len(range(0, tgm.width, tgm.tile_width))
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     flags = kernels.ErrorFlags(src.device)   # checked once, after the timed loop
+    if args.compact:
+        _native.testing_knob("rectify_compact", args.compact).__enter__()
     for r in range(args.reps + 2):
         if r == 2:
             torch.cuda.synchronize()
@@ -65,7 +73,7 @@ def main():
     torch.cuda.synchronize()
     flags.raise_if_set("time_rectify")
     print(f"{os.environ.get('XRS_LIBRARY', 'libxrs.so')}: {ev[0].elapsed_time(ev[1]) / args.reps:.3f} "
-          f"ms per K4+K5+K6{' (fused)' if args.fused else ''}, covered {int(torch.isfinite(out).sum())} px", flush=True)
+          f"ms per K4+K5+K6{' (fused)' if args.fused else ''} res/{args.res_div:g} walk {args.compact}, covered {int(torch.isfinite(out).sum())} px", flush=True)
 
 
 if __name__ == "__main__":

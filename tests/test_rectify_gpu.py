@@ -562,6 +562,12 @@ def test_config4_full_size_matches_oracle():
     np.testing.assert_array_equal(bb, exp_bb)
     assert_bitwise_equal(ij.cpu().numpy(), exp_ij, "ij")
     assert np.sum(~np.isnan(exp_ij[0])) > 30_000_000
+    from xcube_resampling_amd._native import testing_knob
+
+    with testing_knob("rectify_compact", 1):   # the wave-compacted claim walk on every tile
+        ij_c, _ = _device_ij(lon, lat, size, tile, (x0, y0), res, False)
+    assert_bitwise_equal(ij_c.cpu().numpy(), exp_ij, "ij (compacted walk)")
+    del ij_c
     src = torch.from_numpy(var).cuda()
     # the fused pass (K6 inside K5's resolve) is what rectify_dataset runs for
     # its first variable and what the config-4 line times: oracle-pinned here
@@ -629,7 +635,7 @@ def _device_ij_crs(x, y, size, tile, xy_min, res, j_up, crs, names):
     return R._compute_target_source_ij(sgm, tgm, 1e-3), bb
 
 
-# quads covering ~0.3 to ~4 target pixels per side, rotated and sheared, in
+# quads covering ~0.3 to ~8 target pixels per side, rotated and sheared, in
 # degrees near (5, 60) and in UTM metres near (5e5, 6.6e6) with 20-30 m pixels
 FORM_CASES = [
     # (seed, scale, angle_deg, projected, jitter, j_up)
@@ -639,6 +645,10 @@ FORM_CASES = [
     (3, 2.4, 61.0, True, 0.3, False),
     (4, 3.7, 5.0, False, 0.0, False),
     (5, 1.0, 0.0, True, 0.0, True),    # lattice: source points on target pixel centres
+    # quads of 30-90 target pixels: windows above kLaneWindow, walked by the
+    # whole wave on the quad's forms
+    (6, 5.5, 23.0, False, 0.1, False),
+    (7, 8.0, -47.0, True, 0.2, True),
 ]
 
 
@@ -668,11 +678,13 @@ def _form_case_geometry(seed, scale, angle, projected, jitter):
 def test_claim_forms_match_oracle_geometries(seed, scale, angle, projected, jitter, j_up):
     """K5a decides each (quad, pixel) test from float32 affine forms with a
     per-quad error bound and the reference's exact float64 test inside the
-    band: over quads from 0.35 to 3.7 target pixels wide, rotated, jittered,
+    band: over quads from 0.35 to 8 target pixels wide (the widest walked by
+    the whole wave), rotated, jittered,
     in degrees and in UTM metres (large coordinates, small pixels), and a
     lattice whose source points sit on target pixel centres, ij == the C
     oracle bit for bit — and again with the band widened 3000-fold (the
-    exact-test path taken by a large share of the tests)."""
+    exact-test path taken by a large share of the tests), and with every tile
+    forced through the wave-compacted walk and through the per-lane walk."""
     from oracle import gridmapping_ref as gref
     from xcube_resampling_amd._native import testing_knob
 
@@ -689,3 +701,11 @@ def test_claim_forms_match_oracle_geometries(seed, scale, angle, projected, jitt
     with testing_knob("rectify_margin", 3000):
         ij_w, _ = _device_ij_crs(x, y, size, tile, xy_min, res, j_up, crs, names)
     assert_bitwise_equal(ij_w.cpu().numpy(), exp_ij, "ij (widened band)")
+    # every tile through the wave-compacted walk, and every tile per lane
+    for mode, name in ((1, "compacted"), (2, "per-lane")):
+        with testing_knob("rectify_compact", mode):
+            ij_c, _ = _device_ij_crs(x, y, size, tile, xy_min, res, j_up, crs, names)
+            assert_bitwise_equal(ij_c.cpu().numpy(), exp_ij, f"ij ({name} walk)")
+            with testing_knob("rectify_margin", 3000):
+                ij_c, _ = _device_ij_crs(x, y, size, tile, xy_min, res, j_up, crs, names)
+            assert_bitwise_equal(ij_c.cpu().numpy(), exp_ij, f"ij ({name} walk, widened band)")

@@ -169,7 +169,8 @@ MAX_PROJ_STEPS = 4
 
 TESTING_KNOBS = {"reproject_band": 1, "reproject_blocks_per_cu": 2, "affine_generic": 3,
                  "rectify_exact": 4, "rectify_margin": 5,
-                 "rectify_plain_keys": 7, "proj_two_step": 8}   # 6: retired (K1's column-group deal, round 5)
+                 "rectify_plain_keys": 7, "proj_two_step": 8,
+                 "rectify_compact": 9}   # 6: retired (K1's column-group deal, round 5)
 
 
 class testing_knob:

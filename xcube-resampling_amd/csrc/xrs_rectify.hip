@@ -697,6 +697,18 @@ constexpr double kMargin = 1e-9;
 constexpr int kClaimThreads = 256;   // K5a block: 4 waves
 constexpr int kClaimOffsLds = 1023;  // tiles whose offsets are copied to LDS (8 KB)
 constexpr int kLaneWindow = 16;  // windows up to this many pixels: walked per lane
+// the compacted walk: windows up to kCompactWindow pixels, the list of a
+// wave-row's window pixels marked in LDS (kMarkCap positions, one byte each:
+// owner lane + 1 at the owner's first position, 0 elsewhere)
+constexpr int kCompactWindow = 48;
+constexpr int kMarkCap = 64 * kCompactWindow;
+// the product's choice, per launch: the compacted walk when the target has
+// at least kCompactRatio pixels per source quad (dst_h dst_w / ((h - 1)
+// (w - 1)): the quads' mean area in target pixels over the fraction of the
+// target they cover).  Config 4: 2.32 (1.67 / 0.72), where the per-lane walk
+// is 0.5-1.5 % faster; 2.81 (a 1.1x finer target) already favours
+// compaction, 3.6 (1.25x) by 14 % (profiles/r06m_claim_walk_choice_ab.log).
+constexpr double kCompactRatio = 2.6;
 constexpr double kEps64 = 0x1p-52;
 constexpr double kEps32 = 0x1p-23;
 constexpr double kMaxFormMargin = 1e-3;   // larger bound: exact test at every pixel
@@ -849,6 +861,50 @@ __device__ inline uint32_t walk_pair(const TriForms2& F, int n, float wn) {
   return W;
 }
 
+// walk_pair's code of one window pixel (af, bf) (column, row from the window
+// origin), for the compacted walk
+__device__ inline int pixel_code(const TriForms2& F, float af, float bf) {
+  const f32x2 av = {af, af}, bv = {bf, bf};
+  const f32x2 u = __builtin_elementwise_fma(bv, F.uj, __builtin_elementwise_fma(av, F.ui, F.u0));
+  const f32x2 v = __builtin_elementwise_fma(bv, F.vj, __builtin_elementwise_fma(av, F.vi, F.v0));
+  const f32x2 w = __builtin_elementwise_fma(bv, F.wj, __builtin_elementwise_fma(av, F.wi, F.w0));
+  const float ha = fminf(u.x, fminf(v.x, w.x)), hb = fminf(u.y, fminf(v.y, w.y));
+  const bool a_in = ha >= 0.0f, a_near = ha >= F.thr.x;
+  return a_in ? 1 : (!a_near && hb >= 0.0f) ? 2 : (a_near || hb >= F.thr.y) ? 3 : 0;
+}
+
+// Wave-wide inclusive scans (64 lanes) by DPP: row_shr 1, 2, 4, 8 within each
+// row of 16 lanes (bound_ctrl: lanes shifted in from outside the row read 0),
+// then row_bcast:15 (lane 15 of rows 0 / 2 into rows 1 / 3) and row_bcast:31
+// (lane 31 into rows 2, 3).  Identity 0: v >= 0 for the max scan.
+template <int CTRL, int ROWS, bool BC>
+__device__ inline int32_t dpp0(int32_t v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, ROWS, 0xF, BC);
+}
+__device__ inline int32_t wave_scan_add(int32_t v) {
+  v += dpp0<0x111, 0xF, true>(v);
+  v += dpp0<0x112, 0xF, true>(v);
+  v += dpp0<0x114, 0xF, true>(v);
+  v += dpp0<0x118, 0xF, true>(v);
+  v += dpp0<0x142, 0xA, false>(v);
+  v += dpp0<0x143, 0xC, false>(v);
+  return v;
+}
+__device__ inline int32_t wave_scan_max(int32_t v) {
+  v = max(v, dpp0<0x111, 0xF, true>(v));
+  v = max(v, dpp0<0x112, 0xF, true>(v));
+  v = max(v, dpp0<0x114, 0xF, true>(v));
+  v = max(v, dpp0<0x118, 0xF, true>(v));
+  v = max(v, dpp0<0x142, 0xA, false>(v));
+  v = max(v, dpp0<0x143, 0xC, false>(v));
+  return v;
+}
+
+// lane (addr / 4)'s value (ds_bpermute: every source lane must be active)
+__device__ inline float bperm_f32(int32_t addr, float v) {
+  return __int_as_float(__builtin_amdgcn_ds_bpermute(addr, __float_as_int(v)));
+}
+
 // The trim pad of a quad's window (floors of the corners' extreme pixel
 // units q, rectify.py:500-526): only pixels whose centre i + 0.5 lies within
 // `pad` of [qx0, qx1] x [qy0, qy1] can be hit.  A point the reference counts
@@ -962,11 +1018,23 @@ __device__ inline void claim_exact_lane(const RectArgs& a, const TileInfo& ti, i
 // LDS_OFFS: offsets staged in LDS (up to kClaimOffsLds tiles) or read from
 // HBM; YPOS: the sign of y_scale (j axis up), which decides whether the
 // corners' min or max y gives the first window row — a launch constant
-template <bool LDS_OFFS, bool YPOS>
+// COMPACT: the wave-compacted walk (else per lane), chosen per launch
+template <bool LDS_OFFS, bool YPOS, bool COMPACT>
 __global__ void __launch_bounds__(kClaimThreads, 4)   // <= 128 VGPRs: 4 waves per SIMD
 rectify_claim_kernel(RectArgs a) {
   __shared__ int64_t offs_s[kClaimOffsLds + 1];
+  // the compacted walk, per wave (no block synchronisation): owner marks of
+  // the list positions and the owners' forms (12 KB + 16 KB)
+  constexpr int kW = COMPACT ? kClaimThreads / 64 : 1;
+  __shared__ uint8_t mark_s[kW][COMPACT ? kMarkCap : 1];
+  __shared__ f32x2 forms_s[kW][COMPACT ? 8 : 1][64];
   const int lane = threadIdx.x & 63;
+  uint8_t* const mark = mark_s[COMPACT ? threadIdx.x >> 6 : 0];
+  f32x2 (*const forms)[64] = forms_s[COMPACT ? threadIdx.x >> 6 : 0];
+  if (COMPACT)
+    for (int32_t k = lane; k < kMarkCap; k += 64) mark[k] = 0;   // cleared after each row
+  // windows above kWin pixels leave the walks (the wave-wide exact walk)
+  constexpr int kWin = COMPACT ? kCompactWindow : kLaneWindow;
   constexpr bool lds_offs = LDS_OFFS;
   if (lds_offs)
     for (int64_t t = threadIdx.x; t <= a.ntiles; t += kClaimThreads) offs_s[t] = a.chunk_offs[t];
@@ -1057,6 +1125,8 @@ rectify_claim_kernel(RectArgs a) {
       bool slow = false;     // window not decided fast: claim_exact_lane
       uint32_t hit = 0, hit_b = 0, unsure = 0;   // bit 2k: window pixel k (row-major) hit
                                                   // (hit_b: by triangle B) / undecided
+      int32_t nwalk = 0;     // compacted walk, > 0: the trimmed window's pixels, tested
+                             // by the wave below with the forms F
       if (has_q) {
         // the corners' extreme pixel units (float32, tile-local: |q| is at most
         // a few tile widths for every quad the fast path takes)
@@ -1096,7 +1166,7 @@ rectify_claim_kernel(RectArgs a) {
           int64_t cnt = (int64_t)(ti1 - ti0 + 1) * (tj1 - tj0 + 1);
           bool walk = !empty;
           // (the exact-decision test knob sets an infinite margin: R always)
-          if (pad >= 0.25f || !(a.margin < 0.25) || (!empty && cnt > kLaneWindow)) {
+          if (pad >= 0.25f || !(a.margin < 0.25) || (!empty && cnt > kWin)) {
             walk = false;
             // R from the float64 pixel units (rare: large windows / quads)
             const double dqx0 = qx(fmin(fmin(t0.x, t1.x), fmin(b0.x, b1.x)));
@@ -1117,7 +1187,7 @@ rectify_claim_kernel(RectArgs a) {
                 cnt = (int64_t)(ti1 - ti0 + 1) * (tj1 - tj0 + 1);
                 if (ti0 > ti1 || tj0 > tj1) {
                   // no pixel centre near the quad: nothing to test
-                } else if (cnt > kLaneWindow) {
+                } else if (cnt > kWin) {
                   imin = i0; jmin = j0; nw = i1 - i0 + 1;   // untrimmed: exact test everywhere
                   big_cnt = (int64_t)(i1 - i0 + 1) * (j1 - j0 + 1);   // (a quad without a
                                                                        // triangle is dropped there)
@@ -1149,10 +1219,19 @@ rectify_claim_kernel(RectArgs a) {
             if (st.x < 0 || st.y < 0) {
               slow = true;   // a triangle without a usable bound: exact, untrimmed window
             } else if (st.x | st.y) {
-              const uint32_t W = walk_pair(F, n, wn);
-              hit = (W ^ (W >> 1)) & 0x55555555u;   // codes 1, 2 at bit 2k
-              hit_b = W >> 1;                        // bit 2k: the code's high bit
-              unsure = W & (W >> 1) & 0x55555555u;  // code 3
+              if constexpr (COMPACT) {
+                nwalk = n;
+                // the forms for the compacted walk below (wi, wj are recomputed
+                // there); this wave's previous row has finished reading them
+                forms[0][lane] = F.u0; forms[1][lane] = F.ui; forms[2][lane] = F.uj;
+                forms[3][lane] = F.v0; forms[4][lane] = F.vi; forms[5][lane] = F.vj;
+                forms[6][lane] = F.w0; forms[7][lane] = F.thr;
+              } else {
+                const uint32_t W = walk_pair(F, n, wn);
+                hit = (W ^ (W >> 1)) & 0x55555555u;   // codes 1, 2 at bit 2k
+                hit_b = W >> 1;                        // bit 2k: the code's high bit
+                unsure = W & (W >> 1) & 0x55555555u;  // code 3
+              }
             }
           }
         } else {
@@ -1162,9 +1241,83 @@ rectify_claim_kernel(RectArgs a) {
       const uint32_t key = (uint32_t)qj * a.key_mul + (uint32_t)qi;   // raster order
       // claim keys of the two triangles (tri_bit: the low bit names B)
       const uint32_t key_a = claim_key(a, key, 1), key_b = claim_key(a, key, 2);
+      if constexpr (COMPACT) {
+        // ---- the compacted walk (rectify.py:547-573 for every trimmed window) ----
+        // The lanes' window pixels form one list, pixel k of lane l at P_l + k
+        // (P: exclusive prefix sum of nwalk); the wave tests them 64 at a time,
+        // each lane one pixel of the list with its owner's forms (LDS) and
+        // window (ds_bpermute), so a wave-row costs ceil(sum / 64) steps instead
+        // of the longest window.  The owner of list position g is the last lane
+        // whose window starts at or before g: each owner marks its start (LDS,
+        // cleared again after the row) and a wave max-scan carries it over the
+        // window.  The per-pixel decision is
+        // the per-lane walk's (pixel_code: the same float32 forms at the same
+        // (a, b)), so every claim is the per-lane walk's.
+        const int32_t incl = wave_scan_add(nwalk);
+        const int32_t total = __builtin_amdgcn_readlane(incl, 63);
+        if (total > 0) {   // wave-uniform
+          const int32_t P = incl - nwalk;
+          if (nwalk > 0) mark[P] = (uint8_t)(lane + 1);   // owner's mark
+          __builtin_amdgcn_wave_barrier();   // (one wave's LDS accesses complete in order)
+          // nw (<= 48), n (<= 48) and P (< kMarkCap) of this lane, for its pixels' lanes
+          const uint32_t pk = (uint32_t)nw | ((uint32_t)nwalk << 6) | ((uint32_t)P << 12);
+          const float rnw_self = __builtin_amdgcn_rcpf((float)max(nw, 1));
+          int32_t carry = 0;   // owner + 1 of the list position before this step
+          for (int32_t base = 0; base < total; base += 64) {
+            const int32_t g = base + lane;
+            int32_t m = 0;
+            if (g < total) m = mark[g];
+            m = max(wave_scan_max(m), carry);
+            carry = __builtin_amdgcn_readlane(m, 63);
+            const int32_t o = (m - 1) & 63;   // owner lane (past the list: unused)
+            const int32_t oa = o << 2;        // its bpermute address
+            const uint32_t opk = (uint32_t)__builtin_amdgcn_ds_bpermute(oa, (int32_t)pk);
+            const int32_t oimin = __builtin_amdgcn_ds_bpermute(oa, imin);
+            const int32_t ojmin = __builtin_amdgcn_ds_bpermute(oa, jmin);
+            const float ornw = bperm_f32(oa, rnw_self);
+            const int32_t onw = (int32_t)(opk & 63u), on = (int32_t)((opk >> 6) & 63u);
+            const int32_t k = g - (int32_t)(opk >> 12);
+            if (g < total && m > 0 && k >= 0 && k < on) {
+              // the owner's forms (wi, wj by tri_forms2's own expressions: the
+              // same bits as the owner's)
+              TriForms2 G;
+              G.u0 = forms[0][o]; G.ui = forms[1][o]; G.uj = forms[2][o];
+              G.v0 = forms[3][o]; G.vi = forms[4][o]; G.vj = forms[5][o];
+              G.w0 = forms[6][o]; G.thr = forms[7][o];
+              G.wi = -(G.ui + G.vi); G.wj = -(G.uj + G.vj);
+              // window pixel k: row k / nw, column k % nw (exact in float for
+              // k < 64: the quotient is >= 1/128 from an integer)
+              const int32_t dj = (int32_t)(((float)k + 0.5f) * ornw);
+              const int32_t di = k - dj * onw;
+              int tri = pixel_code(G, (float)di, (float)dj);
+              if (tri != 0) {
+                const uint32_t okey = (uint32_t)qj * a.key_mul + (uint32_t)(qi - lane + o);
+                const int32_t pj = ojmin + dj, pi = oimin + di;   // tile-local pixel
+                if (tri == 3) {   // a pixel centre within the margin of an edge: exact
+                  const Quad Q = load_quad(a, qj, qi - lane + o);
+                  const double dy = ti.y_off + ((double)pj + 0.5) * a.y_scale;
+                  const double dx = ti.x_off + ((double)pi + 0.5) * a.x_scale;
+                  tri = tri_choice_exact(Q, dx, dy, umin, uvmax);
+                }
+                if (tri) {
+                  const uint32_t ck = claim_key(a, okey, tri);
+                  uint32_t* tile_keys = a.keys + (int64_t)ti.r0 * a.dst_w + ti.c0;
+                  if (a.narrow)   // 32-bit byte offsets from the wave-uniform tile base
+                    atomicMin(reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(tile_keys) +
+                                                          (((uint32_t)pj * (uint32_t)a.dst_w +
+                                                            (uint32_t)pi) << 2)), ck);
+                  else
+                    atomicMin(tile_keys + (int64_t)pj * a.dst_w + pi, ck);
+                }
+              }
+            }
+          }
+          if (nwalk > 0) mark[P] = 0;   // after this wave's reads of the row (in order)
+        }
+      }
       // claims: the window pixels hit (row k / nw, column k % nw: exact in float
       // for k < 16, the quotient is >= 1/32 from an integer)
-      if (hit | unsure) {
+      if (!COMPACT && (hit | unsure)) {
         const float rnw = 1.0f / (float)nw;
         uint32_t* tile_keys = a.keys + (int64_t)ti.r0 * a.dst_w + ti.c0;
         if (a.narrow) {
@@ -1743,26 +1896,37 @@ int rectify_ij_impl(const char* what, const double* x, const double* y, int64_t 
   if (!keys_ready)   // else filled by K4 (xrs_ij_bboxes_fill) or the caller
     XRS_HIP_CHECK(hipMemsetAsync(keys, 0xFF, (size_t)(dst_h * dst_w) * sizeof(uint32_t), st));
   {
+    // the walk (kCompactRatio); tests: xrs_testing_set(XRS_TESTING_RECTIFY_COMPACT,
+    // 1 / 2) takes the compacted / the per-lane walk whatever the ratio
+    const int64_t force = xrs_testing_value(XRS_TESTING_RECTIFY_COMPACT);
+    const bool compact = force == 1 ||
+        (force != 2 && (double)dst_h * (double)dst_w >= kCompactRatio * (double)(h - 1) * (double)(w - 1));
     // as many blocks as are resident at once (fewer when the caller knows a
     // smaller strip count)
     constexpr int wpb = kClaimThreads / 64;
-    static const int resident =   // one device model per process
-        resident_blocks(reinterpret_cast<const void*>(rectify_claim_kernel<true, false>),
-                        kClaimThreads);
-    const int64_t want = max_chunks > 0 ? (max_chunks + wpb - 1) / wpb : resident;
-    const int nb = (int)min(want, (int64_t)resident);
-    const bool ypos = y_scale > 0;
-    if (ntiles <= kClaimOffsLds) {
-      if (ypos)
-        hipLaunchKernelGGL((rectify_claim_kernel<true, true>), dim3(nb), dim3(kClaimThreads), 0, st, a);
+    static const int resident[2] = {   // one device model per process
+        resident_blocks(reinterpret_cast<const void*>(rectify_claim_kernel<true, false, false>),
+                        kClaimThreads),
+        resident_blocks(reinterpret_cast<const void*>(rectify_claim_kernel<true, false, true>),
+                        kClaimThreads)};
+    const bool ypos = y_scale > 0, lds = ntiles <= kClaimOffsLds;
+    auto launch = [&](auto mode) {
+      constexpr bool C = decltype(mode)::value;
+      const int64_t want = max_chunks > 0 ? (max_chunks + wpb - 1) / wpb : resident[C];
+      const int nb = (int)min(want, (int64_t)resident[C]);
+      if (lds && ypos)
+        hipLaunchKernelGGL((rectify_claim_kernel<true, true, C>), dim3(nb), dim3(kClaimThreads), 0, st, a);
+      else if (lds)
+        hipLaunchKernelGGL((rectify_claim_kernel<true, false, C>), dim3(nb), dim3(kClaimThreads), 0, st, a);
+      else if (ypos)
+        hipLaunchKernelGGL((rectify_claim_kernel<false, true, C>), dim3(nb), dim3(kClaimThreads), 0, st, a);
       else
-        hipLaunchKernelGGL((rectify_claim_kernel<true, false>), dim3(nb), dim3(kClaimThreads), 0, st, a);
-    } else {
-      if (ypos)
-        hipLaunchKernelGGL((rectify_claim_kernel<false, true>), dim3(nb), dim3(kClaimThreads), 0, st, a);
-      else
-        hipLaunchKernelGGL((rectify_claim_kernel<false, false>), dim3(nb), dim3(kClaimThreads), 0, st, a);
-    }
+        hipLaunchKernelGGL((rectify_claim_kernel<false, false, C>), dim3(nb), dim3(kClaimThreads), 0, st, a);
+    };
+    if (compact)
+      launch(std::true_type{});
+    else
+      launch(std::false_type{});
     XRS_HIP_CHECK(hipGetLastError());
   }
   const int nb2 = grid_blocks(256 * 32, 1, 1 << 24);
