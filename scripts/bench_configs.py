@@ -1,6 +1,6 @@
 """Secondary measurement lines: BASELINE.json configs 1-4.
 
-    python scripts/bench_configs.py [--configs 1,2,3,4] [--steps K] [--cpu-seconds S]
+    python scripts/bench_configs.py [--configs 1,2,2u,3,3f,4,4f] [--steps K] [--cpu-seconds S]
 
 bench.py measures the headline metric (config 5 on one GPU per slice); this
 script measures the other configurations the same way — inputs resident in
@@ -178,7 +178,7 @@ def issue_pmc(kernels=("claim", "resolve", "ij_bboxes"), timeout=150,
         shutil.rmtree(d, ignore_errors=True)
 
 
-def kernel_times(interp, timeout=150, reps=30):
+def kernel_times(interp, timeout=150, reps=30, res_div=1.0):
     """The fused config-4 pipeline's own kernels (scripts/time_rectify.py
     --fused: K4 + device tiling + claim + resolve with K6 inside), average
     microseconds per launch from one rocprofv3 --kernel-trace --stats child
@@ -195,7 +195,7 @@ def kernel_times(interp, timeout=150, reps=30):
     cmd = ["timeout", "-s", "KILL", str(timeout), prof, "--kernel-trace", "--stats",
            "--output-format", "csv", "-d", d, "-o", "kt", "--", sys.executable,
            os.path.join(ROOT, "scripts", "time_rectify.py"), "--fused", "--interp", interp,
-           "--reps", str(reps)]
+           "--reps", str(reps), "--res-div", str(res_div)]
     r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
     if r.returncode != 0:
         print(f"kernel_times: rocprofv3 failed (rc {r.returncode}):\n{r.stdout[-1500:]}",
@@ -466,8 +466,9 @@ def config3(args, frac=False):
 
 
 # ------------------------------------------------------------------ config 4
-def config4(args):
-    """Rectify a 4000x4800 jittered swath to a ~8.3k x 5.4k EPSG:4326 grid, 512^2 tiles."""
+def config4(args, div=1.0):
+    """Rectify a 4000x4800 jittered swath to a ~8.3k x 5.4k EPSG:4326 grid, 512^2 tiles
+    (div > 1: onto a grid div-fold finer, line "4f": the claim's compacted walk)."""
     import torch
 
     import xcube_resampling_amd as xrs
@@ -484,7 +485,7 @@ def config4(args):
         + rng.normal(0, 0.05 * 0.0027, (h, w))
     lon = 5 + 0.0045 * i + 0.0009 * j + rng.normal(0, 0.05 * 0.0045, (h, w))
     var = rng.random((1, h, w), dtype=np.float32)
-    res = 0.0027
+    res = 0.0027 / div
     x0, y0 = float(np.floor(lon.min() / res) * res), float(np.floor(lat.min() / res) * res)
     tw, th = int(np.ceil((lon.max() - x0) / res)), int(np.ceil((lat.max() - y0) / res))
     tgm = xrs.GridMapping.regular((tw, th), (x0, y0), res, "EPSG:4326", tile_size=512)
@@ -540,7 +541,7 @@ def config4(args):
     S = w * h
     torch.cuda.synchronize()
     issue = issue_pmc()   # the claim is VALU-issue bound, the resolve waits on memory
-    for interp in ("nearest", "bilinear"):
+    for interp in ("nearest", "bilinear") if div == 1.0 else ("nearest",):
         # 20 steps after 5 warm-up passes (5 after 1 let the shader clock's
         # ramp into the timed steps: 0.97 vs 0.90 ms for the same kernels)
         ms, wall = _timed(lambda: pipeline(interp), args.steps, max(5, args.warmup))
@@ -559,11 +560,12 @@ def config4(args):
             best = min(best, time.perf_counter() - t0)
             del ij_c
         cpu_v, dt = npx / best / 1e6, best
-        kt = kernel_times(interp)
+        kt = kernel_times(interp, res_div=div)
         kern = ("fused pipeline: " + ", ".join(f"{k} {v:.1f} us" for k, v in kt.items()) +
                 f" (sum {sum(kt.values()) / 1e3:.3f} ms)") if kt else "fused pipeline"
-        _line(4, f"rectify {interp}: 4000x4800 jittered swath (f64 lon/lat, f32 var) -> "
-                 f"{tgm.width}x{tgm.height} EPSG:4326 res 0.0027, 512^2 tiles "
+        _line(4 if div == 1.0 else "4f",
+              f"rectify {interp}: 4000x4800 jittered swath (f64 lon/lat, f32 var) -> "
+                 f"{tgm.width}x{tgm.height} EPSG:4326 res {res:.6g}, 512^2 tiles "
                  "(K4 bbox + device tiling + K5 with K6 fused, end to end, coordinates "
                  "resident in HBM)",
               npx, ms, wall, 16 * S + 4 * S + 4 * npx,
@@ -576,7 +578,7 @@ def config4(args):
                "unfused": {"k5_claim_resolve_ms": round(k5_ms, 4),
                            "k6_ms": round(lines[interp], 4), "pipeline_ms": round(sep_ms, 4)},
                "issue": issue})
-    flags.raise_if_set("config 4")
+    flags.raise_if_set("config 4" if div == 1.0 else "config 4f")
 
 
 def main():
@@ -588,7 +590,7 @@ def main():
     args = ap.parse_args()
     for c in args.configs.split(","):
         {"1": config1, "2": config2, "2u": config2u, "3": config3, "3f": config3f,
-         "4": config4}[c.strip()](args)
+         "4": config4, "4f": lambda a: config4(a, 2.0)}[c.strip()](args)
 
 
 if __name__ == "__main__":

@@ -18,7 +18,7 @@ timeout -k 10 600 python -u bench.py --gpus 1 --warmup 5 --steps 20 > $OUT/bench
 cut -c1-300 $OUT/bench_w5.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o bench -- python3 bench.py --no-cpu-baseline --no-traffic --no-f64 --warmup 5 > $OUT/bench_prof.json 2> $OUT/bench_prof.err || exit $?
 cut -c1-200 $OUT/bench_prof.json
-timeout -k 10 900 python -u scripts/bench_configs.py --configs 1,2,2u,3,3f,4 --cpu-seconds 6 > $OUT/configs.jsonl 2> $OUT/configs.err || { tail -20 $OUT/configs.err; exit 1; }
+timeout -k 10 900 python -u scripts/bench_configs.py --configs 1,2,2u,3,3f,4,4f --cpu-seconds 6 > $OUT/configs.jsonl 2> $OUT/configs.err || { tail -20 $OUT/configs.err; exit 1; }
 cut -c1-160 $OUT/configs.jsonl
 timeout -k 10 300 python -u scripts/rehearse_bands.py > $OUT/bands.jsonl 2> $OUT/bands.err || exit $?
 cut -c1-200 $OUT/bands.jsonl
