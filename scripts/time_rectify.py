@@ -72,8 +72,11 @@ def main():
     ev[1].record()
     torch.cuda.synchronize()
     flags.raise_if_set("time_rectify")
+    bits = out.contiguous().view(torch.int32).to(torch.int64)   # output checksum (bits)
+    csum = int((bits * (torch.arange(bits.numel(), device=bits.device).view(bits.shape) % 1009 + 1)).sum())
     print(f"{os.environ.get('XRS_LIBRARY', 'libxrs.so')}: {ev[0].elapsed_time(ev[1]) / args.reps:.3f} "
-          f"ms per K4+K5+K6{' (fused)' if args.fused else ''} res/{args.res_div:g} walk {args.compact}, covered {int(torch.isfinite(out).sum())} px", flush=True)
+          f"ms per K4+K5+K6{' (fused)' if args.fused else ''} res/{args.res_div:g} walk {args.compact}, covered {int(torch.isfinite(out).sum())} px, "
+          f"checksum {csum}", flush=True)
 
 
 if __name__ == "__main__":
