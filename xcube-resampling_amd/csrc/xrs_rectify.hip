@@ -1470,7 +1470,9 @@ rectify_var_kernel(const double* __restrict__ ij, int64_t ij_sn, int64_t dst_h, 
 // column of the item's rows and issues the key loads of all its rows, then the
 // winning quads' corner loads of all its rows, before any arithmetic — three
 // dependent memory round trips per kResolveRows pixels instead of per pixel.
-constexpr int kResolveRows = 3;
+// 2 rows per thread (items of 128 x 8 target pixels) since late round 6:
+// resolve 272-275 vs 277-280 us with 3 (profiles/r06r_k4_grid_strips_ab.log)
+constexpr int kResolveRows = 2;
 
 // A variable sampled by the resolve pass itself (K6 fused into K5b: the
 // first variable of a rectification needs no ij image round trip through HBM).
@@ -1825,8 +1827,15 @@ extern "C" int xrs_ij_bboxes_fill(const double* x, const double* y, int64_t h, i
   const int64_t lds = (ntx > 0 ? 16 * (ntx + nty) : 32 * nboxes) + 16 * nboxes;
   if (ntx > 0) {   // a tile grid: block-wise (ij_bboxes_block_kernel)
     const int64_t nwave = ((w + 63) / 64) * ((h + kBoxBlockRows - 1) / kBoxBlockRows);
-    const int nbb = grid_blocks(nwave, kThreads / 64, 256 * 8);
-    if (lds <= 48 * 1024)
+    // as many blocks as are resident at once: each wave walks its blocks in
+    // turn (a grid of twice that — 2048 blocks — left a tail of waves with
+    // one block more: K4 95-98 vs 101-102 us at config 4, r06q / r06r)
+    const bool shared = lds <= 48 * 1024;
+    const int nres = resident_blocks(shared ? reinterpret_cast<const void*>(ij_bboxes_block_kernel<true>)
+                                            : reinterpret_cast<const void*>(ij_bboxes_block_kernel<false>),
+                                     kThreads, shared ? (size_t)lds : 0);
+    const int nbb = grid_blocks(nwave, kThreads / 64, nres);
+    if (shared)
       hipLaunchKernelGGL(ij_bboxes_block_kernel<true>, dim3(nbb), dim3(kThreads), (size_t)lds, st,
                          a);
     else
