@@ -1,0 +1,37 @@
+# Round 6, twentieth pass: the resolve at 7 waves per SIMD (p2r7: 261.9 vs
+# 276.1 us in gpu_r06_s.sh) again, at 8 (p2r8: 64 VGPRs, 7 spilled), and p2r7
+# with 16384 / 4096 blocks instead of 8192 (r7g16k, r7g4k); the unfused
+# pass (ij image + K6) for p2r7 too.
+#   bash scripts/gpu_r06_t.sh OUTDIR
+export TMPDIR=/tmp
+O=${1:-gpurun_out/r06t}; mkdir -p $O
+ARMS="p2r7 p2r8 r7g16k r7g4k"
+for arm in $ARMS; do
+  XRS_LIBRARY=probe/$arm/pkg/lib/libxrs.so timeout -k 10 300 python -u -m pytest tests/test_rectify_gpu.py -m gpu -q -x --timeout 200 --timeout-method thread > $O/pytest_$arm.log 2>&1; rc=$?
+  echo "$arm parity: $(tail -1 $O/pytest_$arm.log)"
+  [ $rc -eq 0 ] || { echo "$arm pytest status $rc"; exit $rc; }
+done
+for interp in nearest bilinear; do
+  for pass in 1 2 3; do
+    for arm in product $ARMS; do
+      L=xcube-resampling_amd/lib/libxrs.so
+      [ $arm = product ] || L=probe/$arm/pkg/lib/libxrs.so
+      XRS_LIBRARY=$L timeout -k 10 180 python -u scripts/time_rectify.py --fused --reps 20 --interp $interp > $O/t_${arm}_${interp}_$pass.log 2>&1 || exit $?
+      echo "$arm $interp $pass $(grep 'ms per' $O/t_${arm}_${interp}_$pass.log)"
+    done
+  done
+done
+for pass in 1 2; do
+  for arm in product p2r7; do
+    L=xcube-resampling_amd/lib/libxrs.so
+    [ $arm = product ] || L=probe/$arm/pkg/lib/libxrs.so
+    XRS_LIBRARY=$L timeout -k 10 180 python -u scripts/time_rectify.py --reps 20 > $O/tu_${arm}_$pass.log 2>&1 || exit $?
+    echo "$arm unfused $pass $(grep 'ms per' $O/tu_${arm}_$pass.log)"
+  done
+done
+for arm in product $ARMS; do
+  L=xcube-resampling_amd/lib/libxrs.so
+  [ $arm = product ] || L=probe/$arm/pkg/lib/libxrs.so
+  XRS_LIBRARY=$L timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d $O/ks_$arm -o ks -- python3 scripts/time_rectify.py --fused --reps 10 > $O/ks_$arm.log 2>&1 || exit $?
+  echo "$arm nearest"; python3 scripts/kstats.py $(find $O/ks_$arm -name "*kernel_stats.csv" | head -1) claim resolve bboxes
+done

@@ -1570,12 +1570,14 @@ __device__ inline void sample_rows(const double* fi, const double* fj, int nr,
   }
 }
 
-// Five waves per SIMD (96 VGPRs; 3 values spill to scratch outside the pixel
-// loop): 1.131-1.135 vs 1.156-1.162 ms per config-4 pass at four
-// (profiles/r04_rectify_lb5_ab.log).  Round 3 found 5 slower when the kernel
-// needed 125 VGPRs; 32-bit quad indices and conversions brought it to 98.
+// Seven waves per SIMD with the triangle in the key (TRI: 72 VGPRs, 2 values
+// spilled outside the pixel loop), five otherwise.  Round 4 found 5 faster
+// than 4 (1.131-1.135 vs 1.156-1.162 ms per config-4 pass,
+// profiles/r04_rectify_lb5_ab.log); with 2 rows per thread (late round 6) the
+// TRI kernels need 72-77 VGPRs: 7 waves 259-267 vs 275-280 us at 5, 6 waves no
+// faster, 8 (7 VGPRs spilled) 333 us (profiles/r06s_*, r06t_*).
 template <typename T, bool FUSE, int INTERP, bool TRI>   // TRI: a.tri_bit (compile time)
-__global__ void __launch_bounds__(kThreads, 5)
+__global__ void __launch_bounds__(kThreads, TRI ? 7 : 5)
 rectify_resolve_kernel(RectArgs a, FusedVar fv) {
   const int64_t n = a.dst_h * a.dst_w;
   const T tfill = FUSE ? Conv<T>::from_f64(fv.fill) : T{};
@@ -1938,7 +1940,10 @@ int rectify_ij_impl(const char* what, const double* x, const double* y, int64_t 
       launch(std::false_type{});
     XRS_HIP_CHECK(hipGetLastError());
   }
-  const int nb2 = grid_blocks(256 * 32, 1, 1 << 24);
+  // 16384 blocks (items of 128 x 8 pixels dealt grid-stride; config 4: ~2.7
+  // items per block): resolve 259 vs 267 us with 8192, 4096 280, 32768 260,
+  // 65536 271 (profiles/r06t_*, r06u_*)
+  const int nb2 = grid_blocks(256 * 64, 1, 1 << 24);
   auto resolve = [&](auto tri) -> int {
     constexpr bool TRI = decltype(tri)::value;
     if (!fv) {
