@@ -652,8 +652,11 @@ constexpr double kMargin = 1e-9;
 // next row's points are requested before this row's tests); the quad to its
 // right takes the right-hand corners from the next lane (DPP wave shift) and,
 // walking down, a row's bottom corners become the next row's top corners in
-// registers.  Strips are dealt round-robin to the waves of a grid sized to be
-// resident at once (no tail of late blocks).  A dynamic work counter costs
+// registers.  Strips are dealt round-robin to the waves of the grid: for the
+// per-lane walk a grid of 8x the resident blocks (one strip per wave at
+// config 4, so the hardware dispatcher balances the CUs — a resident grid,
+// 4-5 strips per wave, left a tail: claim 505 vs 466-472 us), for the
+// compacted walk the resident grid (its LDS marks are cleared per block).  A dynamic work counter costs
 // more than it balances: one global atomic per strip on one address
 // serialises at its L2 channel (measured 0.45 vs 0.12 ms for the bare strip
 // loop at config 4); staging a strip's points in LDS (rows then never wait on
@@ -709,6 +712,7 @@ constexpr int kMarkCap = 64 * kCompactWindow;
 // is 0.5-1.5 % faster; 2.81 (a 1.1x finer target) already favours
 // compaction, 3.6 (1.25x) by 14 % (profiles/r06m_claim_walk_choice_ab.log).
 constexpr double kCompactRatio = 2.6;
+constexpr int kClaimGridMul = 8;   // the per-lane walk's grid: 8 x the resident blocks
 constexpr double kEps64 = 0x1p-52;
 constexpr double kEps32 = 0x1p-23;
 constexpr double kMaxFormMargin = 1e-3;   // larger bound: exact test at every pixel
@@ -1912,8 +1916,13 @@ int rectify_ij_impl(const char* what, const double* x, const double* y, int64_t 
     const int64_t force = xrs_testing_value(XRS_TESTING_RECTIFY_COMPACT);
     const bool compact = force == 1 ||
         (force != 2 && (double)dst_h * (double)dst_w >= kCompactRatio * (double)(h - 1) * (double)(w - 1));
-    // as many blocks as are resident at once (fewer when the caller knows a
-    // smaller strip count)
+    // the grid: the compacted walk on as many blocks as are resident at once;
+    // the per-lane walk on kClaimGridMul times that, so that the strips (dealt
+    // round-robin to the waves) come one per wave and the dispatcher balances
+    // the CUs instead of a resident wave's fixed share of 4-5 strips (config
+    // 4: claim 466-472 vs 505 us, profiles/r06v_*, r06w_*; 2x slower than
+    // resident, 4x 482 us; the compacted walk slower off the resident grid);
+    // fewer blocks when the caller knows a smaller strip count
     constexpr int wpb = kClaimThreads / 64;
     static const int resident[2] = {   // one device model per process
         resident_blocks(reinterpret_cast<const void*>(rectify_claim_kernel<true, false, false>),
@@ -1923,8 +1932,9 @@ int rectify_ij_impl(const char* what, const double* x, const double* y, int64_t 
     const bool ypos = y_scale > 0, lds = ntiles <= kClaimOffsLds;
     auto launch = [&](auto mode) {
       constexpr bool C = decltype(mode)::value;
-      const int64_t want = max_chunks > 0 ? (max_chunks + wpb - 1) / wpb : resident[C];
-      const int nb = (int)min(want, (int64_t)resident[C]);
+      const int64_t cap = (int64_t)resident[C] * (C ? 1 : kClaimGridMul);
+      const int64_t want = max_chunks > 0 ? (max_chunks + wpb - 1) / wpb : cap;
+      const int nb = (int)min(want, cap);
       if (lds && ypos)
         hipLaunchKernelGGL((rectify_claim_kernel<true, true, C>), dim3(nb), dim3(kClaimThreads), 0, st, a);
       else if (lds)
