@@ -1049,8 +1049,13 @@ rectify_claim_kernel(RectArgs a) {
   const int64_t nchunks = lds_offs ? offs_s[a.ntiles] : a.chunk_offs[a.ntiles];
   const double umin = -a.uv_delta, uvmax = 1.0 + 2 * a.uv_delta;
   const int64_t nwaves = (int64_t)gridDim.x * (kClaimThreads / 64);
-  for (int64_t c = (int64_t)blockIdx.x * (kClaimThreads / 64) + (threadIdx.x >> 6); c < nchunks;
-       c += nwaves) {
+  // the compacted walk takes each strip in two halves of kStripH / 2 quad rows
+  // (work unit c2: strip c2 >> 1, half c2 & 1), the per-lane walk whole strips
+  constexpr int kHalves = COMPACT ? 2 : 1;
+  for (int64_t c2 = (int64_t)blockIdx.x * (kClaimThreads / 64) + (threadIdx.x >> 6);
+       c2 < nchunks * kHalves; c2 += nwaves) {
+    const int64_t c = c2 / kHalves;
+    const int32_t half = (int32_t)(c2 - c * kHalves);
     int64_t lo = 0, hi = a.ntiles;   // last t with offs[t] <= c (c is wave-uniform)
     if (lds_offs) {
       while (hi - lo > 1) {
@@ -1083,10 +1088,11 @@ rectify_claim_kernel(RectArgs a) {
     const bool has_pt = pcol <= nq_i;
     const bool has_q = lane < kStripW && pcol < nq_i;  // quad (row, pcol) exists
     const int32_t qi = ti.si0 + pcol;
-    const int32_t r0 = cy * kStripH;
-    const int32_t r_end = min(r0 + kStripH, nq_j);
-    if (r0 >= r_end) {   // wave-uniform: a strip past the window (inconsistent offsets)
-      if (lane == 0) atomicOr(a.err_flags, XRS_EFLAG_STATE);
+    const int32_t r0 = cy * kStripH + half * (kStripH / kHalves);
+    const int32_t r_end = min(r0 + kStripH / kHalves, nq_j);
+    if (r0 >= r_end) {   // wave-uniform: a strip past the window (inconsistent offsets),
+                         // or the empty second half of a short strip
+      if (half == 0 && lane == 0) atomicOr(a.err_flags, XRS_EFLAG_STATE);
       continue;
     }
     auto load_pt = [&](int32_t qj) {
